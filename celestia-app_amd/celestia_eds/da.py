@@ -1,0 +1,136 @@
+"""pkg/da surface (pkg/da/data_availability_header.go) over the device library.
+
+  ExtendShares(shares)            :65-75   -> one device pass (RS + NMT roots)
+  NewDataAvailabilityHeader(eds)  :44-63
+  DataAvailabilityHeader          :33-41, Hash :92-108, ValidateBasic :134-162,
+                                  IsZero :164-170, SquareSize :205-207, Equals :86-88
+  MinDataAvailabilityHeader       :179-190, MinShares :193-196
+  SquareSize / RoundUpPowerOfTwo  :205-215
+"""
+import ctypes
+import math
+
+import numpy as np
+
+from . import _lib
+from ._lib import CelError
+from .rsmt2d import ExtendedDataSquare
+
+SHARE_SIZE = _lib.SHARE_SIZE
+MIN_SQUARE_SIZE = 1                # appconsts.MinSquareSize
+DEFAULT_SQUARE_SIZE_UPPER_BOUND = 128  # appconsts.DefaultSquareSizeUpperBound
+MAX_EXTENDED_SQUARE_WIDTH = DEFAULT_SQUARE_SIZE_UPPER_BOUND * 2
+MIN_EXTENDED_SQUARE_WIDTH = MIN_SQUARE_SIZE * 2
+TAIL_PADDING_NAMESPACE = b"\xff" * 28 + b"\xfe"
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def RoundUpPowerOfTwo(n):
+    r = 1
+    while r < n:
+        r <<= 1
+    return r
+
+
+def SquareSize(n):
+    return RoundUpPowerOfTwo(int(math.ceil(math.sqrt(n))))
+
+
+def _is_pow2(n):
+    return n > 0 and (n & (n - 1)) == 0
+
+
+def _extend(shares, ctx=None, order_check=True):
+    ctx = ctx or _lib.default_context()
+    n = len(shares)
+    if not _is_pow2(n):
+        raise CelError(_lib.ENOTPOW2, f"number of shares is not a power of 2: got {n}")
+    if isinstance(shares, np.ndarray):
+        ods = np.ascontiguousarray(shares, np.uint8).reshape(-1)
+    else:
+        ods = np.frombuffer(b"".join(bytes(s) for s in shares), np.uint8).copy()
+    k = SquareSize(n)
+    eds = np.zeros((2 * k, 2 * k, SHARE_SIZE), np.uint8)
+    rr = np.zeros((2 * k, _lib.NMT_NODE_SIZE), np.uint8)
+    cr = np.zeros((2 * k, _lib.NMT_NODE_SIZE), np.uint8)
+    dah = np.zeros(32, np.uint8)
+    ctx.check(ctx.lib.cel_extend_shares(ctx.handle, _p(ods), n, SHARE_SIZE, _p(eds), _p(rr), _p(cr), _p(dah),
+                                        _lib.FLAG_ORDER_CHECK if order_check else 0))
+    out = ExtendedDataSquare(eds, rr, cr, ctx=ctx)
+    out._dah = dah.tobytes()
+    return out
+
+
+def ExtendShares(shares):
+    """da.ExtendShares: [][]byte (k*k shares) -> *rsmt2d.ExtendedDataSquare."""
+    return _extend(shares)
+
+
+class DataAvailabilityHeader:
+    def __init__(self, RowRoots=None, ColumnRoots=None):
+        self.RowRoots = list(RowRoots or [])
+        self.ColumnRoots = list(ColumnRoots or [])
+        self.hash = b""
+
+    def Hash(self):
+        if self.hash:
+            return self.hash
+        ctx = _lib.default_context()
+        w = len(self.RowRoots)
+        out = np.zeros(32, np.uint8)
+        if w != len(self.ColumnRoots) or any(len(r) != _lib.NMT_NODE_SIZE for r in self.RowRoots + self.ColumnRoots):
+            raise CelError(_lib.EINVAL, "DAH roots must be 90-byte NMT roots with as many rows as columns")
+        rr = np.frombuffer(b"".join(self.RowRoots), np.uint8).copy() if w else np.zeros(1, np.uint8)
+        cr = np.frombuffer(b"".join(self.ColumnRoots), np.uint8).copy() if w else np.zeros(1, np.uint8)
+        ctx.check(ctx.lib.cel_dah_hash(ctx.handle, _p(rr), _p(cr), w, _p(out)))
+        self.hash = out.tobytes()
+        return self.hash
+
+    def String(self):
+        return self.Hash().hex().upper()
+
+    def Equals(self, other):
+        return self.Hash() == other.Hash()
+
+    def IsZero(self):
+        return len(self.ColumnRoots) == 0 or len(self.RowRoots) == 0
+
+    def SquareSize(self):
+        return len(self.RowRoots) // 2
+
+    def ValidateBasic(self):
+        if len(self.ColumnRoots) < MIN_EXTENDED_SQUARE_WIDTH or len(self.RowRoots) < MIN_EXTENDED_SQUARE_WIDTH:
+            raise CelError(_lib.EINVAL, "minimum valid DataAvailabilityHeader has at least "
+                                        f"{MIN_EXTENDED_SQUARE_WIDTH} row and column roots")
+        if len(self.ColumnRoots) > MAX_EXTENDED_SQUARE_WIDTH or len(self.RowRoots) > MAX_EXTENDED_SQUARE_WIDTH:
+            raise CelError(_lib.EINVAL, "maximum valid DataAvailabilityHeader has at most "
+                                        f"{MAX_EXTENDED_SQUARE_WIDTH} row and column roots")
+        if len(self.ColumnRoots) != len(self.RowRoots):
+            raise CelError(_lib.EINVAL, "unequal number of row and column roots: row "
+                                        f"{len(self.RowRoots)} col {len(self.ColumnRoots)}")
+        if len(self.Hash()) != 32:
+            raise CelError(_lib.EINVAL, f"wrong hash: expected size to be 32 bytes, got {len(self.Hash())} bytes")
+
+
+def NilDataAvailabilityHeaderHash():
+    """(*DataAvailabilityHeader)(nil).Hash() == merkle.HashFromByteSlices(nil)."""
+    return DataAvailabilityHeader().Hash()
+
+
+def NewDataAvailabilityHeader(eds):
+    dah = DataAvailabilityHeader(eds.RowRoots(), eds.ColRoots())
+    dah.Hash()
+    return dah
+
+
+def MinShares():
+    """One tail-padding share (go-square shares.TailPaddingShares(1))."""
+    share = TAIL_PADDING_NAMESPACE + b"\x01" + b"\x00" * 4
+    return [share + b"\x00" * (SHARE_SIZE - len(share))]
+
+
+def MinDataAvailabilityHeader():
+    return NewDataAvailabilityHeader(ExtendShares(MinShares()))

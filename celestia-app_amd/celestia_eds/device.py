@@ -1,0 +1,55 @@
+"""Device-resident batch API (cel_dev_*), for benchmarks and multi-GPU drivers.
+
+PyTorch is used only as plumbing here: device memory (torch.empty on the GPU) and
+the current HIP stream are handed to the C ABI as raw pointers.
+"""
+import ctypes
+
+from . import _lib
+
+NODE = _lib.NMT_NODE_SIZE
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class SquareBatch:
+    """Pre-allocated device buffers for n squares of width k."""
+
+    def __init__(self, n, k, device=0, ctx=None):
+        import torch
+        self.torch = torch
+        self.n, self.k = n, k
+        self.dev = torch.device("cuda", device)
+        self.ctx = ctx or _lib.default_context(device)
+        w = 2 * k
+        self.ods = torch.empty((n, k, k, _lib.SHARE_SIZE), dtype=torch.uint8, device=self.dev)
+        self.eds = torch.empty((n, w, w, _lib.SHARE_SIZE), dtype=torch.uint8, device=self.dev)
+        self.row_roots = torch.empty((n, w, NODE), dtype=torch.uint8, device=self.dev)
+        self.col_roots = torch.empty((n, w, NODE), dtype=torch.uint8, device=self.dev)
+        self.dah = torch.empty((n, 32), dtype=torch.uint8, device=self.dev)
+        self.status = torch.empty((n,), dtype=torch.int32, device=self.dev)
+        ws = self.ctx.lib.cel_dev_workspace_size(k, n)
+        self.work = torch.empty((ws,), dtype=torch.uint8, device=self.dev)
+
+    def stream(self):
+        return ctypes.c_void_p(self.torch.cuda.current_stream(self.dev).cuda_stream)
+
+    def extend_and_commit(self, order_check=True):
+        c = self.ctx
+        c.check(c.lib.cel_dev_extend_batch(c.handle, _ptr(self.ods), self.n, self.k, _ptr(self.eds),
+                                           _ptr(self.row_roots), _ptr(self.col_roots), _ptr(self.dah),
+                                           _ptr(self.status), _ptr(self.work), self.stream(),
+                                           _lib.FLAG_ORDER_CHECK if order_check else 0))
+
+    def extend_only(self):
+        c = self.ctx
+        c.check(c.lib.cel_dev_extend_only(c.handle, _ptr(self.ods), self.n, self.k, _ptr(self.eds), self.stream()))
+
+    def commit_only(self, order_check=True):
+        c = self.ctx
+        c.check(c.lib.cel_dev_commit_only(c.handle, _ptr(self.eds), self.n, self.k, _ptr(self.row_roots),
+                                          _ptr(self.col_roots), _ptr(self.dah), _ptr(self.status),
+                                          _ptr(self.work), self.stream(),
+                                          _lib.FLAG_ORDER_CHECK if order_check else 0))

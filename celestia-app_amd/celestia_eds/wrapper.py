@@ -1,0 +1,74 @@
+"""pkg/wrapper surface (pkg/wrapper/nmt_wrapper.go) over the device library.
+
+ErasuredNamespacedMerkleTree keeps the reference's Push-time checks and errors
+(:93-114) and computes Root (:118-124) on the device: a full axis (2k pushes)
+goes through cel_axis_root, a partial one through cel_nmt_root over the
+namespace-prefixed leaves.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import CelError
+
+PARITY_NAMESPACE = b"\xff" * _lib.NAMESPACE_SIZE
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class ErasuredNamespacedMerkleTree:
+    def __init__(self, square_size, axis_index, ctx=None):
+        if square_size == 0:
+            raise ValueError("cannot create a ErasuredNamespacedMerkleTree of squareSize == 0")
+        self.squareSize = int(square_size)
+        self.axisIndex = int(axis_index)
+        self.shareIndex = 0
+        self.leaves = []  # namespace-prefixed data
+        self.ctx = ctx or _lib.default_context()
+
+    def isQuadrantZero(self):
+        return self.shareIndex < self.squareSize and self.axisIndex < self.squareSize
+
+    def Push(self, data):
+        data = bytes(data)
+        if self.axisIndex + 1 > 2 * self.squareSize or self.shareIndex + 1 > 2 * self.squareSize:
+            raise CelError(_lib.EPUSHPAST, "pushed past predetermined square size: boundary at "
+                                           f"{2 * self.squareSize} index at {self.axisIndex} {self.shareIndex}")
+        if len(data) < _lib.NAMESPACE_SIZE:
+            raise CelError(_lib.ESHORT, "data is too short to contain namespace ID")
+        ns = data[:_lib.NAMESPACE_SIZE] if self.isQuadrantZero() else PARITY_NAMESPACE
+        leaf = ns + data
+        if self.leaves and leaf[:_lib.NAMESPACE_SIZE] < self.leaves[-1][:_lib.NAMESPACE_SIZE]:
+            raise CelError(_lib.EORDER, "pushed data has to be lexicographically ordered by namespace IDs")
+        self.leaves.append(leaf)
+        self.shareIndex += 1
+
+    def Root(self):
+        n = len(self.leaves)
+        out = np.zeros(_lib.NMT_NODE_SIZE, np.uint8)
+        full = (n == 2 * self.squareSize and all(len(l) == _lib.NAMESPACE_SIZE + _lib.SHARE_SIZE
+                                                  for l in self.leaves))
+        if full:
+            cells = np.frombuffer(b"".join(l[_lib.NAMESPACE_SIZE:] for l in self.leaves), np.uint8).copy()
+            self.ctx.check(self.ctx.lib.cel_axis_root(self.ctx.handle, _p(cells), self.squareSize, self.axisIndex,
+                                                      _lib.SHARE_SIZE, _p(out), 0))
+        else:
+            ln = len(self.leaves[0]) if n else _lib.NAMESPACE_SIZE
+            if any(len(l) != ln for l in self.leaves):
+                raise CelError(_lib.EINVAL, "device NMT root needs equal-length leaves")
+            buf = np.frombuffer(b"".join(self.leaves), np.uint8).copy() if n else np.zeros(1, np.uint8)
+            self.ctx.check(self.ctx.lib.cel_nmt_root(self.ctx.handle, _p(buf), n, ln, _p(out), 0))
+        return out.tobytes()
+
+
+def NewErasuredNamespacedMerkleTree(square_size, axis_index):
+    return ErasuredNamespacedMerkleTree(square_size, axis_index)
+
+
+def NewConstructor(square_size):
+    def NewTree(_axis, axis_index):
+        return ErasuredNamespacedMerkleTree(square_size, axis_index)
+    return NewTree

@@ -1,0 +1,570 @@
+// C ABI of the MI355X EDS hot path (include/celestia_eds.h).
+//
+// Host-side mirror of the reference surface, in C++ because the reference host
+// (Go) is compiled code and no Go toolchain is available here:
+//   cel_extend_shares  <- da.ExtendShares + da.NewDataAvailabilityHeader
+//                         (pkg/da/data_availability_header.go:65-75, :44-63)
+//   cel_codec_*        <- rsmt2d.LeoRSCodec (pkg/appconsts/global_consts.go:92)
+//   cel_axis_root      <- wrapper.ErasuredNamespacedMerkleTree Push/Root (pkg/wrapper/nmt_wrapper.go:93-124)
+//   cel_dah_hash       <- DataAvailabilityHeader.Hash (data_availability_header.go:92-108)
+//   cel_repair         <- rsmt2d ExtendedDataSquare.Repair [dep]
+// Every computation runs in the HIP kernels; this layer validates arguments with
+// the reference's error semantics, stages host buffers and orders the launches.
+// There is no CPU fallback: without a usable device every call fails with
+// CEL_EDEVICE.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "cel_internal.hpp"
+
+using namespace cel;
+
+namespace {
+
+enum ScratchSlot { S_IN = 0, S_EDS = 1, S_WORK = 2, S_ROOTS = 3, S_AUX = 4, S_MASK = 5 };
+
+cel_status fail(cel_ctx* ctx, cel_status st, const std::string& msg) {
+  if (ctx) ctx->last_error = msg;
+  return st;
+}
+
+cel_status hip_fail(cel_ctx* ctx, hipError_t e, const char* what) {
+  return fail(ctx, CEL_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+void* scratch(cel_ctx* ctx, int slot, size_t bytes, hipError_t* err) {
+  if (bytes == 0) bytes = 256;
+  if (ctx->scratch_size[slot] >= bytes) return ctx->scratch[slot];
+  if (ctx->scratch[slot]) (void)hipFree(ctx->scratch[slot]);
+  ctx->scratch[slot] = nullptr;
+  ctx->scratch_size[slot] = 0;
+  void* p = nullptr;
+  *err = hipMalloc(&p, bytes);
+  if (*err != hipSuccess) return nullptr;
+  ctx->scratch[slot] = p;
+  ctx->scratch_size[slot] = bytes;
+  return p;
+}
+
+bool is_pow2(uint64_t n) { return n && !(n & (n - 1)); }
+
+// da.SquareSize: RoundUpPowerOfTwo(ceil(sqrt(len))) (data_availability_header.go:205-215)
+uint32_t square_size(uint32_t n) {
+  const uint32_t s = (uint32_t)std::ceil(std::sqrt((double)n));
+  uint32_t r = 1;
+  while (r < s) r <<= 1;
+  return r;
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+hipStream_t pick_stream(cel_ctx* ctx, void* stream) {
+  return stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+}
+
+}  // namespace
+
+extern "C" {
+
+cel_status cel_ctx_create(int device, cel_ctx** out) {
+  if (!out) return CEL_EINVAL;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return CEL_EDEVICE;
+  if (device < 0 || device >= n) return CEL_EINVAL;
+  cel_ctx* ctx = new cel_ctx();
+  ctx->device = device;
+  DeviceGuard g(device);
+  hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = upload_tables(&ctx->tables);
+  if (e != hipSuccess) {
+    cel_ctx_destroy(ctx);
+    return CEL_EDEVICE;
+  }
+  *out = ctx;
+  return CEL_OK;
+}
+
+void cel_ctx_destroy(cel_ctx* ctx) {
+  if (!ctx) return;
+  {
+    DeviceGuard g(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (int i = 0; i < 6; i++)
+      if (ctx->scratch[i]) (void)hipFree(ctx->scratch[i]);
+    free_tables(&ctx->tables);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  }
+  delete ctx;
+}
+
+const char* cel_strerror(cel_status st) {
+  switch (st) {
+    case CEL_OK: return "ok";
+    case CEL_EINVAL: return "invalid argument";
+    case CEL_ENOTPOW2: return "number of shares is not a power of 2";
+    case CEL_ECHUNK: return "chunk size must be a positive multiple of 64";
+    case CEL_ETOOBIG: return "square too large for the device path";
+    case CEL_EORDER: return "invalid push order: namespaces must be non-decreasing";
+    case CEL_ETOOFEW: return "too few shards given";
+    case CEL_EBYZANTINE: return "byzantine data: axis failed re-encoding or root verification";
+    case CEL_EUNREPAIRABLE: return "failed to solve data square";
+    case CEL_EDEVICE: return "HIP device error";
+    case CEL_ENOMEM: return "device out of memory";
+    case CEL_ESHORT: return "data is too short to contain namespace ID";
+    case CEL_EPUSHPAST: return "pushed past predetermined square size";
+    default: return "unknown status";
+  }
+}
+
+const char* cel_last_error(const cel_ctx* ctx) { return ctx ? ctx->last_error.c_str() : ""; }
+
+cel_status cel_device_name(cel_ctx* ctx, char* buf, size_t len) {
+  if (!ctx || !buf || !len) return CEL_EINVAL;
+  hipDeviceProp_t p;
+  if (hipGetDeviceProperties(&p, ctx->device) != hipSuccess) return CEL_EDEVICE;
+  std::snprintf(buf, len, "%s (%s)", p.name, p.gcnArchName);
+  return CEL_OK;
+}
+
+// ------------------------------------------------------------------ squares
+
+size_t cel_dev_workspace_size(uint32_t k, uint32_t n) { return nmt_workspace_size(k, n); }
+
+static cel_status validate_square(cel_ctx* ctx, uint32_t k, uint32_t share_size) {
+  if (share_size != kShare)
+    return fail(ctx, CEL_ECHUNK, "share size must be appconsts.ShareSize (512) on the device path");
+  if (!is_pow2(k)) return fail(ctx, CEL_ENOTPOW2, "square width is not a power of 2: got " + std::to_string(k));
+  if (k > 512) return fail(ctx, CEL_ETOOBIG, "square width " + std::to_string(k) + " exceeds the device path (512)");
+  return CEL_OK;
+}
+
+cel_status cel_dev_extend_only(cel_ctx* ctx, const void* d_ods, uint32_t n, uint32_t k, void* d_eds, void* stream) {
+  if (!ctx || !d_eds || !n) return CEL_EINVAL;
+  cel_status st = validate_square(ctx, k, kShare);
+  if (st) return st;
+  DeviceGuard g(ctx->device);
+  hipError_t e = launch_extend(static_cast<const uint8_t*>(d_ods), static_cast<uint8_t*>(d_eds), k, n, ctx->tables,
+                               pick_stream(ctx, stream));
+  return e == hipSuccess ? CEL_OK : hip_fail(ctx, e, "extend");
+}
+
+cel_status cel_dev_commit_only(cel_ctx* ctx, const void* d_eds, uint32_t n, uint32_t k, void* d_row_roots,
+                               void* d_col_roots, void* d_dah, int32_t* d_status, void* d_work, void* stream,
+                               uint32_t flags) {
+  if (!ctx || !d_eds || !n || !d_row_roots || !d_col_roots || !d_dah || !d_work) return CEL_EINVAL;
+  cel_status st = validate_square(ctx, k, kShare);
+  if (st) return st;
+  DeviceGuard g(ctx->device);
+  hipError_t e = launch_commit(static_cast<const uint8_t*>(d_eds), k, n, static_cast<uint8_t*>(d_row_roots),
+                               static_cast<uint8_t*>(d_col_roots), static_cast<uint8_t*>(d_dah), d_status, d_work,
+                               (flags & CEL_FLAG_ORDER_CHECK) != 0, pick_stream(ctx, stream));
+  return e == hipSuccess ? CEL_OK : hip_fail(ctx, e, "commit");
+}
+
+cel_status cel_dev_extend_batch(cel_ctx* ctx, const void* d_ods, uint32_t n, uint32_t k, void* d_eds,
+                                void* d_row_roots, void* d_col_roots, void* d_dah, int32_t* d_status, void* d_work,
+                                void* stream, uint32_t flags) {
+  cel_status st = cel_dev_extend_only(ctx, d_ods, n, k, d_eds, stream);
+  if (st) return st;
+  return cel_dev_commit_only(ctx, d_eds, n, k, d_row_roots, d_col_roots, d_dah, d_status, d_work, stream, flags);
+}
+
+cel_status cel_extend_batch(cel_ctx* ctx, const uint8_t* ods, uint32_t n, uint32_t k, uint32_t share_size,
+                            uint8_t* eds_out, uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah,
+                            int32_t* status_out, uint32_t flags) {
+  if (!ctx) return CEL_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (!ods || !row_roots || !col_roots || !dah || !n) return fail(ctx, CEL_EINVAL, "nil argument");
+  cel_status st = validate_square(ctx, k, share_size);
+  if (st) return st;
+  DeviceGuard g(ctx->device);
+  const size_t ods_b = (size_t)n * k * k * kShare, eds_b = 4 * ods_b;
+  const size_t roots_b = (size_t)n * 2 * k * kNode;
+  hipError_t e = hipSuccess;
+  uint8_t* d_ods = static_cast<uint8_t*>(scratch(ctx, S_IN, ods_b, &e));
+  if (!d_ods) return fail(ctx, CEL_ENOMEM, "device allocation failed");
+  uint8_t* d_eds = static_cast<uint8_t*>(scratch(ctx, S_EDS, eds_b, &e));
+  if (!d_eds) return fail(ctx, CEL_ENOMEM, "device allocation failed");
+  void* d_work = scratch(ctx, S_WORK, nmt_workspace_size(k, n), &e);
+  if (!d_work) return fail(ctx, CEL_ENOMEM, "device allocation failed");
+  uint8_t* d_out = static_cast<uint8_t*>(scratch(ctx, S_ROOTS, 2 * roots_b + (size_t)n * 32 + (size_t)n * 4, &e));
+  if (!d_out) return fail(ctx, CEL_ENOMEM, "device allocation failed");
+  uint8_t* d_rr = d_out;
+  uint8_t* d_cr = d_out + roots_b;
+  uint8_t* d_dah = d_out + 2 * roots_b;
+  int32_t* d_st = reinterpret_cast<int32_t*>(d_out + 2 * roots_b + (size_t)n * 32);
+  hipStream_t s = ctx->stream;
+  if ((e = hipMemcpyAsync(d_ods, ods, ods_b, hipMemcpyHostToDevice, s)) != hipSuccess) return hip_fail(ctx, e, "H2D");
+  if ((e = launch_extend(d_ods, d_eds, k, n, ctx->tables, s)) != hipSuccess) return hip_fail(ctx, e, "extend");
+  if ((e = launch_commit(d_eds, k, n, d_rr, d_cr, d_dah, d_st, d_work, (flags & CEL_FLAG_ORDER_CHECK) != 0, s)) !=
+      hipSuccess)
+    return hip_fail(ctx, e, "commit");
+  if (eds_out && (e = hipMemcpyAsync(eds_out, d_eds, eds_b, hipMemcpyDeviceToHost, s)) != hipSuccess)
+    return hip_fail(ctx, e, "D2H");
+  std::vector<int32_t> stv(n);
+  if ((e = hipMemcpyAsync(row_roots, d_rr, roots_b, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+      (e = hipMemcpyAsync(col_roots, d_cr, roots_b, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+      (e = hipMemcpyAsync(dah, d_dah, (size_t)n * 32, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+      (e = hipMemcpyAsync(stv.data(), d_st, (size_t)n * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+    return hip_fail(ctx, e, "D2H");
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "sync");
+  cel_status worst = CEL_OK;
+  for (uint32_t i = 0; i < n; i++) {
+    if (status_out) status_out[i] = stv[i];
+    if (stv[i] != CEL_OK && worst == CEL_OK) worst = stv[i];
+  }
+  if (worst == CEL_EORDER) return fail(ctx, CEL_EORDER, "invalid push order: leaf namespaces must be non-decreasing");
+  return worst;
+}
+
+cel_status cel_extend_shares(cel_ctx* ctx, const uint8_t* shares, uint32_t n_shares, uint32_t share_size,
+                             uint8_t* eds_out, uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah, uint32_t flags) {
+  if (!ctx) return CEL_EINVAL;
+  // data_availability_header.go:67-69
+  if (!is_pow2(n_shares))
+    return fail(ctx, CEL_ENOTPOW2, "number of shares is not a power of 2: got " + std::to_string(n_shares));
+  const uint32_t k = square_size(n_shares);
+  if ((uint64_t)k * k != n_shares)
+    // rsmt2d.ComputeExtendedDataSquare rejects a share count that is not a perfect square
+    return fail(ctx, CEL_EINVAL, "number of chunks must be a square number: got " + std::to_string(n_shares));
+  return cel_extend_batch(ctx, shares, 1, k, share_size, eds_out, row_roots, col_roots, dah, nullptr, flags);
+}
+
+// -------------------------------------------------------------------- codec
+
+uint64_t cel_codec_max_chunks(void) { return 32768ull * 32768ull; }
+const char* cel_codec_name(void) { return "Leopard"; }
+cel_status cel_codec_validate_chunk_size(uint32_t len) {
+  return (len == 0 || (len % 64) != 0) ? CEL_ECHUNK : CEL_OK;
+}
+
+cel_status cel_codec_encode(cel_ctx* ctx, const uint8_t* data, uint32_t n, uint32_t len, uint8_t* parity) {
+  if (!ctx) return CEL_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (!data || !parity || !n) return fail(ctx, CEL_EINVAL, "nil argument");
+  if (cel_codec_validate_chunk_size(len)) return fail(ctx, CEL_ECHUNK, "shard size must be a multiple of 64");
+  if (!is_pow2(n)) return fail(ctx, CEL_ENOTPOW2, "number of data shards is not a power of 2");
+  if (n > kMaxGf16Width) return fail(ctx, CEL_ETOOBIG, "too many shards for the device path");
+  DeviceGuard g(ctx->device);
+  hipError_t e = hipSuccess;
+  const size_t b = (size_t)n * len;
+  uint8_t* d_in = static_cast<uint8_t*>(scratch(ctx, S_IN, b, &e));
+  uint8_t* d_out = static_cast<uint8_t*>(scratch(ctx, S_EDS, b, &e));
+  if (!d_in || !d_out) return fail(ctx, CEL_ENOMEM, "device allocation failed");
+  hipStream_t s = ctx->stream;
+  if ((e = hipMemcpyAsync(d_in, data, b, hipMemcpyHostToDevice, s)) != hipSuccess) return hip_fail(ctx, e, "H2D");
+  RsGeom gm{};
+  gm.in = d_in;
+  gm.out = d_out;
+  gm.in_sq = gm.out_sq = b;
+  gm.in_axis = gm.out_axis = b;
+  gm.in_shard = gm.out_shard = len;
+  gm.n = n;
+  gm.len = len;
+  gm.axes = 1;
+  gm.nsq = 1;
+  if ((e = launch_rs_encode(gm, ctx->tables, s)) != hipSuccess) return hip_fail(ctx, e, "encode");
+  if ((e = hipMemcpyAsync(parity, d_out, b, hipMemcpyDeviceToHost, s)) != hipSuccess) return hip_fail(ctx, e, "D2H");
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "sync");
+  return CEL_OK;
+}
+
+cel_status cel_codec_decode(cel_ctx* ctx, uint8_t* shards, const uint8_t* present, uint32_t n, uint32_t len) {
+  if (!ctx) return CEL_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (!shards || !present || !n) return fail(ctx, CEL_EINVAL, "nil argument");
+  if (cel_codec_validate_chunk_size(len)) return fail(ctx, CEL_ECHUNK, "shard size must be a multiple of 64");
+  if (!is_pow2(n)) return fail(ctx, CEL_ENOTPOW2, "number of data shards is not a power of 2");
+  if (n > 1024) return fail(ctx, CEL_ETOOBIG, "too many shards for the device decoder");
+  uint32_t have = 0;
+  for (uint32_t i = 0; i < 2 * n; i++) have += present[i] ? 1 : 0;
+  if (have == 2 * n) return CEL_OK;
+  if (have < n) return fail(ctx, CEL_ETOOFEW, "too few shards given");
+  DeviceGuard g(ctx->device);
+  hipError_t e = hipSuccess;
+  const size_t b = (size_t)2 * n * len;
+  uint8_t* d_sh = static_cast<uint8_t*>(scratch(ctx, S_IN, b, &e));
+  uint8_t* d_pr = static_cast<uint8_t*>(scratch(ctx, S_MASK, 2 * n, &e));
+  if (!d_sh || !d_pr) return fail(ctx, CEL_ENOMEM, "device allocation failed");
+  hipStream_t s = ctx->stream;
+  if ((e = hipMemcpyAsync(d_sh, shards, b, hipMemcpyHostToDevice, s)) != hipSuccess ||
+      (e = hipMemcpyAsync(d_pr, present, 2 * n, hipMemcpyHostToDevice, s)) != hipSuccess)
+    return hip_fail(ctx, e, "H2D");
+  if ((e = launch_rs_decode(d_sh, d_pr, 1, n, len, ctx->tables, nullptr, s)) != hipSuccess)
+    return hip_fail(ctx, e, "decode");
+  if ((e = hipMemcpyAsync(shards, d_sh, b, hipMemcpyDeviceToHost, s)) != hipSuccess) return hip_fail(ctx, e, "D2H");
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "sync");
+  return CEL_OK;
+}
+
+// -------------------------------------------------------------------- trees
+
+cel_status cel_axis_root(cel_ctx* ctx, const uint8_t* cells, uint32_t k, uint32_t axis_index, uint32_t share_size,
+                         uint8_t* root_out, uint32_t flags) {
+  if (!ctx) return CEL_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (!cells || !root_out || !k) return fail(ctx, CEL_EINVAL, "nil argument");
+  if (share_size != kShare) return fail(ctx, CEL_ECHUNK, "share size must be 512 on the device path");
+  if (axis_index + 1 > 2 * k)  // nmt_wrapper.go:94-96
+    return fail(ctx, CEL_EPUSHPAST, "pushed past predetermined square size: boundary at " + std::to_string(2 * k) +
+                                        " index at " + std::to_string(axis_index) + " 0");
+  if (flags & CEL_FLAG_ORDER_CHECK) {
+    // honest nmt push order over the Q0 part of the axis (the rest carries the max namespace)
+    if (axis_index < k)
+      for (uint32_t i = 1; i < k; i++)
+        if (std::memcmp(cells + (size_t)i * kShare, cells + (size_t)(i - 1) * kShare, kNs) < 0)
+          return fail(ctx, CEL_EORDER, "invalid push order: namespace of leaf " + std::to_string(i) +
+                                           " is smaller than the previous one");
+  }
+  DeviceGuard g(ctx->device);
+  hipError_t e = hipSuccess;
+  const size_t b = (size_t)2 * k * kShare;
+  uint8_t* d_c = static_cast<uint8_t*>(scratch(ctx, S_IN, b, &e));
+  void* d_w = scratch(ctx, S_WORK, axis_root_workspace_size(k), &e);
+  uint8_t* d_r = static_cast<uint8_t*>(scratch(ctx, S_ROOTS, 256, &e));
+  if (!d_c || !d_w || !d_r) return fail(ctx, CEL_ENOMEM, "device allocation failed");
+  hipStream_t s = ctx->stream;
+  if ((e = hipMemcpyAsync(d_c, cells, b, hipMemcpyHostToDevice, s)) != hipSuccess) return hip_fail(ctx, e, "H2D");
+  if ((e = launch_axis_root(d_c, k, axis_index, d_r, d_w, s)) != hipSuccess) return hip_fail(ctx, e, "axis root");
+  if ((e = hipMemcpyAsync(root_out, d_r, kNode, hipMemcpyDeviceToHost, s)) != hipSuccess) return hip_fail(ctx, e, "D2H");
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "sync");
+  return CEL_OK;
+}
+
+cel_status cel_nmt_root(cel_ctx* ctx, const uint8_t* leaves, uint32_t n, uint32_t leaf_len, uint8_t* root_out,
+                        uint32_t flags) {
+  if (!ctx) return CEL_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if ((!leaves && n) || !root_out) return fail(ctx, CEL_EINVAL, "nil argument");
+  if (n && leaf_len < kNs) return fail(ctx, CEL_ESHORT, "data is too short to contain namespace ID");
+  if ((flags & CEL_FLAG_ORDER_CHECK) && n > 1)
+    for (uint32_t i = 1; i < n; i++)
+      if (std::memcmp(leaves + (size_t)i * leaf_len, leaves + (size_t)(i - 1) * leaf_len, kNs) < 0)
+        return fail(ctx, CEL_EORDER, "invalid push order: namespace of leaf " + std::to_string(i) +
+                                         " is smaller than the previous one");
+  DeviceGuard g(ctx->device);
+  hipError_t e = hipSuccess;
+  const size_t b = (size_t)n * leaf_len;
+  uint8_t* d_l = static_cast<uint8_t*>(scratch(ctx, S_IN, b, &e));
+  void* d_w = scratch(ctx, S_WORK, nmt_root_workspace_size(n), &e);
+  uint8_t* d_r = static_cast<uint8_t*>(scratch(ctx, S_ROOTS, 256, &e));
+  if (!d_l || !d_w || !d_r) return fail(ctx, CEL_ENOMEM, "device allocation failed");
+  hipStream_t s = ctx->stream;
+  if (b && (e = hipMemcpyAsync(d_l, leaves, b, hipMemcpyHostToDevice, s)) != hipSuccess) return hip_fail(ctx, e, "H2D");
+  if ((e = launch_nmt_root(d_l, n, leaf_len, d_r, d_w, s)) != hipSuccess) return hip_fail(ctx, e, "nmt root");
+  if ((e = hipMemcpyAsync(root_out, d_r, kNode, hipMemcpyDeviceToHost, s)) != hipSuccess) return hip_fail(ctx, e, "D2H");
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "sync");
+  return CEL_OK;
+}
+
+cel_status cel_dah_hash(cel_ctx* ctx, const uint8_t* row_roots, const uint8_t* col_roots, uint32_t w, uint8_t* out) {
+  if (!ctx) return CEL_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (!out || (w && (!row_roots || !col_roots))) return fail(ctx, CEL_EINVAL, "nil argument");
+  if (2 * (size_t)w > 2048) return fail(ctx, CEL_ETOOBIG, "too many roots for the device DAH kernel");
+  DeviceGuard g(ctx->device);
+  hipError_t e = hipSuccess;
+  const size_t b = (size_t)2 * w * kNode;
+  uint8_t* d_items = static_cast<uint8_t*>(scratch(ctx, S_IN, b, &e));
+  void* d_w = scratch(ctx, S_WORK, merkle_workspace_size(2 * w), &e);
+  uint8_t* d_o = static_cast<uint8_t*>(scratch(ctx, S_ROOTS, 256, &e));
+  if (!d_items || !d_w || !d_o) return fail(ctx, CEL_ENOMEM, "device allocation failed");
+  hipStream_t s = ctx->stream;
+  if (w) {
+    if ((e = hipMemcpyAsync(d_items, row_roots, (size_t)w * kNode, hipMemcpyHostToDevice, s)) != hipSuccess ||
+        (e = hipMemcpyAsync(d_items + (size_t)w * kNode, col_roots, (size_t)w * kNode, hipMemcpyHostToDevice, s)) !=
+            hipSuccess)
+      return hip_fail(ctx, e, "H2D");
+  }
+  if ((e = launch_merkle_root(d_items, 2 * w, kNode, d_o, d_w, s)) != hipSuccess) return hip_fail(ctx, e, "merkle");
+  if ((e = hipMemcpyAsync(out, d_o, 32, hipMemcpyDeviceToHost, s)) != hipSuccess) return hip_fail(ctx, e, "D2H");
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "sync");
+  return CEL_OK;
+}
+
+// ------------------------------------------------------------------- repair
+
+// rsmt2d Repair crossword loop. The control loop (which axes are solvable) runs
+// on the host over the presence mask; decoding, re-encoding, byte comparisons and
+// root computation run on the device over the EDS kept resident.
+namespace {
+
+struct RepairBufs {
+  uint8_t* eds;
+  uint8_t* mask;
+  uint8_t* dense;
+  uint8_t* dmask;
+  uint8_t* tmp;
+  int32_t* idx;
+  int32_t* flags;
+  uint32_t* roots;
+  void* work;
+};
+
+// Verify (and for solve=true, decode first) a list of axes. Returns CEL_OK, or
+// CEL_EBYZANTINE with *bad set to the list entry that failed.
+cel_status process_axes(cel_ctx* ctx, const RepairBufs& b, uint32_t k, int is_col, const std::vector<int32_t>& list,
+                        const uint8_t* exp_roots, bool solve, int32_t* bad) {
+  const uint32_t W = 2 * k, na = (uint32_t)list.size();
+  hipStream_t s = ctx->stream;
+  hipError_t e;
+  if ((e = hipMemcpyAsync(b.idx, list.data(), na * 4, hipMemcpyHostToDevice, s)) != hipSuccess) return hip_fail(ctx, e, "H2D");
+  if ((e = hipMemsetAsync(b.flags, 0, na * 4, s)) != hipSuccess) return hip_fail(ctx, e, "memset");
+  if ((e = launch_gather_axes(b.eds, b.mask, W, b.idx, is_col, na, b.dense, b.dmask, s)) != hipSuccess)
+    return hip_fail(ctx, e, "gather");
+  if (solve) {
+    if ((e = launch_rs_decode(b.dense, b.dmask, na, k, kShare, ctx->tables, nullptr, s)) != hipSuccess)
+      return hip_fail(ctx, e, "decode");
+    // re-encode the data half and compare with the parity half (rsmt2d verifyEncoding)
+    RsGeom g{};
+    g.in = b.dense;
+    g.in_sq = (uint64_t)na * W * kShare;
+    g.in_axis = (uint64_t)W * kShare;
+    g.in_shard = kShare;
+    g.out = b.tmp;
+    g.out_sq = (uint64_t)na * k * kShare;
+    g.out_axis = (uint64_t)k * kShare;
+    g.out_shard = kShare;
+    g.n = k;
+    g.len = kShare;
+    g.axes = na;
+    g.nsq = 1;
+    if ((e = launch_rs_encode(g, ctx->tables, s)) != hipSuccess) return hip_fail(ctx, e, "re-encode");
+    if ((e = launch_cmp(b.tmp, (uint64_t)k * kShare, b.dense + (uint64_t)k * kShare, (uint64_t)W * kShare,
+                        (uint64_t)k * kShare, na, b.flags, s)) != hipSuccess)
+      return hip_fail(ctx, e, "compare");
+  }
+  if ((e = launch_axes_roots(b.dense, k, b.idx, na, b.roots, b.work, s)) != hipSuccess) return hip_fail(ctx, e, "roots");
+  std::vector<int32_t> flags(na);
+  std::vector<uint32_t> roots((size_t)na * kNodeWords);
+  if ((e = hipMemcpyAsync(flags.data(), b.flags, na * 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+      (e = hipMemcpyAsync(roots.data(), b.roots, roots.size() * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+    return hip_fail(ctx, e, "D2H");
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "sync");
+  for (uint32_t a = 0; a < na; a++) {
+    const uint8_t* got = reinterpret_cast<const uint8_t*>(&roots[(size_t)a * kNodeWords]);
+    if (flags[a] || std::memcmp(got, exp_roots + (size_t)list[a] * kNode, kNode) != 0) {
+      *bad = list[a];
+      return CEL_EBYZANTINE;
+    }
+  }
+  if (solve && (e = launch_scatter_axes(b.eds, b.mask, W, b.idx, is_col, na, b.dense, s)) != hipSuccess)
+    return hip_fail(ctx, e, "scatter");
+  return CEL_OK;
+}
+
+}  // namespace
+
+cel_status cel_repair(cel_ctx* ctx, uint8_t* eds, uint8_t* present, uint32_t k, uint32_t share_size,
+                      const uint8_t* row_roots, const uint8_t* col_roots, int32_t* bad_axis, int32_t* bad_index) {
+  if (!ctx) return CEL_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (!eds || !present || !row_roots || !col_roots) return fail(ctx, CEL_EINVAL, "nil argument");
+  cel_status st = validate_square(ctx, k, share_size);
+  if (st) return st;
+  if (k > 512) return fail(ctx, CEL_ETOOBIG, "square too wide for the device decoder");
+  if (bad_axis) *bad_axis = -1;
+  if (bad_index) *bad_index = -1;
+  DeviceGuard g(ctx->device);
+  const uint32_t W = 2 * k;
+  const size_t cells = (size_t)W * W, eds_b = cells * kShare;
+  hipError_t e = hipSuccess;
+  RepairBufs b{};
+  b.eds = static_cast<uint8_t*>(scratch(ctx, S_EDS, eds_b, &e));
+  b.dense = static_cast<uint8_t*>(scratch(ctx, S_IN, eds_b, &e));
+  b.tmp = static_cast<uint8_t*>(scratch(ctx, S_AUX, eds_b / 2 + cells + 3 * (size_t)W * 4 + 256, &e));
+  b.work = scratch(ctx, S_WORK, axes_roots_workspace_size(k, W), &e);
+  b.roots = static_cast<uint32_t*>(scratch(ctx, S_ROOTS, (size_t)W * kNodeWords * 4 + 4 * kNodeWords * 4 * W, &e));
+  b.mask = static_cast<uint8_t*>(scratch(ctx, S_MASK, 2 * cells + 256, &e));
+  if (!b.eds || !b.dense || !b.tmp || !b.work || !b.roots || !b.mask)
+    return fail(ctx, CEL_ENOMEM, "device allocation failed");
+  b.dmask = b.mask + ((cells + 255) & ~(size_t)255);
+  uint8_t* aux = b.tmp + eds_b / 2;
+  b.idx = reinterpret_cast<int32_t*>(aux);
+  b.flags = reinterpret_cast<int32_t*>(aux + (size_t)W * 4);
+  hipStream_t s = ctx->stream;
+  std::vector<uint8_t> hm(cells);
+  for (size_t i = 0; i < cells; i++) hm[i] = present[i] ? 1 : 0;
+  if ((e = hipMemcpyAsync(b.eds, eds, eds_b, hipMemcpyHostToDevice, s)) != hipSuccess ||
+      (e = hipMemcpyAsync(b.mask, hm.data(), cells, hipMemcpyHostToDevice, s)) != hipSuccess)
+    return hip_fail(ctx, e, "H2D");
+  auto count = [&](int is_col, uint32_t i) {
+    uint32_t c = 0;
+    for (uint32_t j = 0; j < W; j++) c += is_col ? hm[(size_t)j * W + i] : hm[(size_t)i * W + j];
+    return c;
+  };
+  auto byz = [&](int is_col, int32_t idx) {
+    if (bad_axis) *bad_axis = is_col;
+    if (bad_index) *bad_index = idx;
+    return fail(ctx, CEL_EBYZANTINE, std::string("byzantine ") + (is_col ? "column" : "row") + " " +
+                                         std::to_string(idx));
+  };
+  // prerepairSanityCheck: complete axes must match their roots.
+  for (int is_col = 0; is_col < 2; is_col++) {
+    std::vector<int32_t> list;
+    for (uint32_t i = 0; i < W; i++)
+      if (count(is_col, i) == W) list.push_back((int32_t)i);
+    if (list.empty()) continue;
+    int32_t bad = -1;
+    st = process_axes(ctx, b, k, is_col, list, is_col ? col_roots : row_roots, false, &bad);
+    if (st == CEL_EBYZANTINE) return byz(is_col, bad);
+    if (st) return st;
+  }
+  // crossword: alternate rows and columns until solved or stuck
+  for (;;) {
+    bool progress = false;
+    for (int is_col = 0; is_col < 2; is_col++) {
+      std::vector<int32_t> list;
+      for (uint32_t i = 0; i < W; i++) {
+        const uint32_t c = count(is_col, i);
+        if (c >= k && c < W) list.push_back((int32_t)i);
+      }
+      if (list.empty()) continue;
+      int32_t bad = -1;
+      st = process_axes(ctx, b, k, is_col, list, is_col ? col_roots : row_roots, true, &bad);
+      if (st == CEL_EBYZANTINE) return byz(is_col, bad);
+      if (st) return st;
+      for (int32_t i : list)
+        for (uint32_t j = 0; j < W; j++) {
+          if (is_col) hm[(size_t)j * W + i] = 1;
+          else hm[(size_t)i * W + j] = 1;
+        }
+      progress = true;
+    }
+    size_t have = 0;
+    for (size_t i = 0; i < cells; i++) have += hm[i];
+    if (have == cells) break;
+    if (!progress) return fail(ctx, CEL_EUNREPAIRABLE, "failed to solve data square");
+  }
+  // Every axis solved along one direction must also match on the other.
+  for (int is_col = 0; is_col < 2; is_col++) {
+    std::vector<int32_t> list(W);
+    for (uint32_t i = 0; i < W; i++) list[i] = (int32_t)i;
+    int32_t bad = -1;
+    st = process_axes(ctx, b, k, is_col, list, is_col ? col_roots : row_roots, false, &bad);
+    if (st == CEL_EBYZANTINE) return byz(is_col, bad);
+    if (st) return st;
+  }
+  if ((e = hipMemcpyAsync(eds, b.eds, eds_b, hipMemcpyDeviceToHost, s)) != hipSuccess) return hip_fail(ctx, e, "D2H");
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "sync");
+  for (size_t i = 0; i < cells; i++) present[i] = 1;
+  return CEL_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,104 @@
+// Internal declarations shared by the HIP kernels and the C-ABI host layer.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <mutex>
+#include <string>
+
+#include "../../include/celestia_eds.h"
+
+namespace cel {
+
+constexpr uint32_t kShare = CEL_SHARE_SIZE;
+constexpr uint32_t kNs = CEL_NAMESPACE_SIZE;
+constexpr uint32_t kNode = CEL_NMT_NODE_SIZE;
+constexpr uint32_t kNodeWords = 24;  // 90-byte node padded to 96 B (24 dwords) on the device
+constexpr uint32_t kMaxGf8Width = 128;   // k <= 128 -> 2k <= 256 shards -> GF(2^8)
+constexpr uint32_t kMaxGf16Width = 2048; // LDS holds 2048 shards x 64 B per workgroup
+
+// One RS encode launch: `axes` independent axes of n data shards each, for `nsq`
+// squares. Shard i of axis a of square s lives at
+//   in + s*in_sq + a*in_axis + i*in_shard        (len bytes)
+// and its parity shard i goes to out + s*out_sq + a*out_axis + i*out_shard.
+struct RsGeom {
+  const uint8_t* in;
+  uint8_t* out;
+  uint64_t in_sq, in_axis, in_shard;
+  uint64_t out_sq, out_axis, out_shard;
+  // Optional copy of the data shards (the row pass writes Q0 into the EDS while it
+  // has them in registers): dcopy + s*dc_sq + a*dc_axis + i*dc_shard. nullptr = none.
+  uint8_t* dcopy;
+  uint64_t dc_sq, dc_axis, dc_shard;
+  uint32_t n;     // data shards per axis (power of two)
+  uint32_t len;   // bytes per shard (multiple of 64)
+  uint32_t axes;  // axes per square
+  uint32_t nsq;   // squares
+};
+
+struct DeviceTables {
+  uint32_t* tw8 = nullptr;     // [255][8] GF(2^8) twiddle product tables, indexed by skew index
+  uint16_t* exp16 = nullptr;   // [65536]
+  uint16_t* log16 = nullptr;   // [65536]
+  uint16_t* skew16 = nullptr;  // [65535]
+  uint32_t* mul8 = nullptr;    // [256][8] GF(2^8) product tables indexed by log value (decoder)
+};
+
+hipError_t upload_tables(DeviceTables* t);
+void free_tables(DeviceTables* t);
+
+// Kernel launchers (rs_kernels.hip / nmt_kernels.hip). All asynchronous on `s`.
+hipError_t launch_rs_encode(const RsGeom& g, const DeviceTables& t, hipStream_t s);
+// Full 2D extension of nsq squares: Q0 rows -> Q1, then all 2k columns -> Q2|Q3.
+// ods == nullptr means Q0 is already in place inside eds.
+hipError_t launch_extend(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t nsq,
+                         const DeviceTables& t, hipStream_t s);
+
+// NMT + DAH over resident EDSs. work: scratch of nmt_workspace_size(k, nsq) bytes.
+size_t nmt_workspace_size(uint32_t k, uint32_t nsq);
+hipError_t launch_commit(const uint8_t* eds, uint32_t k, uint32_t nsq, uint8_t* row_roots,
+                         uint8_t* col_roots, uint8_t* dah, int32_t* status, void* work,
+                         bool order_check, hipStream_t s);
+// One erasured axis root (cells contiguous) or plain NMT root over leaves.
+hipError_t launch_axis_root(const uint8_t* cells, uint32_t k, uint32_t axis, uint8_t* root,
+                            void* work, hipStream_t s);
+size_t axis_root_workspace_size(uint32_t k);
+hipError_t launch_nmt_root(const uint8_t* leaves, uint32_t n, uint32_t leaf_len, uint8_t* root,
+                           void* work, hipStream_t s);
+size_t nmt_root_workspace_size(uint32_t n);
+// RFC-6962 root over n items of item_len bytes (DataAvailabilityHeader.Hash).
+hipError_t launch_merkle_root(const uint8_t* items, uint32_t n, uint32_t item_len, uint8_t* out,
+                              void* work, hipStream_t s);
+size_t merkle_workspace_size(uint32_t n);
+
+// Repair helpers (repair_kernels.hip, nmt_kernels.hip).
+hipError_t launch_gather_axes(const uint8_t* eds, const uint8_t* mask, uint32_t W, const int32_t* idx, int is_col,
+                              uint32_t naxes, uint8_t* dense, uint8_t* dmask, hipStream_t s);
+hipError_t launch_scatter_axes(uint8_t* eds, uint8_t* mask, uint32_t W, const int32_t* idx, int is_col,
+                               uint32_t naxes, const uint8_t* dense, hipStream_t s);
+hipError_t launch_cmp(const uint8_t* x, uint64_t xstride, const uint8_t* y, uint64_t ystride, uint64_t bytes,
+                      uint32_t naxes, int32_t* flags, hipStream_t s);
+size_t axes_roots_workspace_size(uint32_t k, uint32_t naxes);
+hipError_t launch_axes_roots(const uint8_t* cells, uint32_t k, const int32_t* axis_idx, uint32_t naxes,
+                             uint32_t* roots, void* work, hipStream_t s);
+
+// Erasure decode of `naxes` axes of 2n shards each, gathered into a dense
+// [naxes][2n][len] buffer with a [naxes][2n] present mask. In place.
+hipError_t launch_rs_decode(uint8_t* shards, const uint8_t* present, uint32_t naxes, uint32_t n,
+                            uint32_t len, const DeviceTables& t, void* work, hipStream_t s);
+size_t decode_workspace_size(uint32_t naxes, uint32_t n);
+
+}  // namespace cel
+
+// The opaque context of the C ABI.
+struct cel_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  cel::DeviceTables tables;
+  std::string last_error;
+  // Grow-only device scratch (reused across calls on this ctx).
+  void* scratch[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  size_t scratch_size[6] = {0, 0, 0, 0, 0, 0};
+};

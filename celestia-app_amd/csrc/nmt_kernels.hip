@@ -1,0 +1,699 @@
+// Namespaced Merkle tree roots and the DataAvailabilityHeader hash on gfx950.
+//
+// Replaces, for the 4k axes of a 2k x 2k EDS:
+//   rsmt2d RowRoots/ColRoots [dep] -> wrapper.ErasuredNamespacedMerkleTree.Push/Root
+//   (pkg/wrapper/nmt_wrapper.go:93-124) -> nmt v0.22.0 HashLeaf / HashNode with
+//   IgnoreMaxNamespace (text copy: test/util/malicious/hasher.go:196-310), and
+//   DataAvailabilityHeader.Hash (pkg/da/data_availability_header.go:92-108) ->
+//   go-square/merkle RFC-6962.
+//
+// Work decomposition (one message per lane everywhere):
+//   k_leaf   : one lane per EDS cell. A cell's row leaf and column leaf are the same
+//              bytes (the Q0 test of nmt_wrapper.go:138-140 is symmetric), so each
+//              leaf is hashed once: 4k^2 x 9 compressions instead of the reference's
+//              8k^2 x 9. Also checks the honest push order on Q0.
+//   k_level  : one lane per inner node of one tree level, all 4k trees at once.
+//   k_top    : one wave per tree for the last <= 64 nodes (LDS, no launch per level).
+//   k_dah    : one workgroup per square, RFC-6962 over the 4k roots.
+// Nodes live on the device as 96-byte records (90 B node + 6 zero bytes) = 24 dwords.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+
+#include "cel_internal.hpp"
+#include "sha256_device.hpp"
+
+namespace cel {
+
+struct Node {
+  uint32_t d[kNodeWords];
+};
+
+__device__ __forceinline__ void load_node(const uint32_t* p, uint32_t (&n)[kNodeWords]) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    const uint4 v = q[i];
+    n[4 * i] = v.x; n[4 * i + 1] = v.y; n[4 * i + 2] = v.z; n[4 * i + 3] = v.w;
+  }
+}
+
+__device__ __forceinline__ void store_node(uint32_t* p, const uint32_t (&n)[kNodeWords]) {
+  uint4* q = reinterpret_cast<uint4*>(p);
+#pragma unroll
+  for (int i = 0; i < 6; i++) q[i] = make_uint4(n[4 * i], n[4 * i + 1], n[4 * i + 2], n[4 * i + 3]);
+}
+
+// Node dwords 14..23 from the 8 big-endian digest words (digest = node bytes 58..89).
+// nd14 keeps its low 16 bits (the last two max-namespace bytes).
+__device__ __forceinline__ void put_digest(uint32_t (&nd)[kNodeWords], const uint32_t (&st)[8]) {
+  uint32_t sw[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) sw[i] = bswap32(st[i]);
+  nd[14] = (nd[14] & 0xFFFFu) | (sw[0] << 16);
+#pragma unroll
+  for (int i = 15; i <= 21; i++) nd[i] = __builtin_amdgcn_alignbyte(sw[i - 14], sw[i - 15], 2);
+  nd[22] = sw[7] >> 16;
+  nd[23] = 0;
+}
+
+// --------------------------------------------------------------------- leaves
+
+// Leaf message: 0x00 || ns(29) || share(512) = 542 B -> 9 blocks.
+// s = the share's little-endian dwords; ns = share[0:29] for Q0 cells, 0xFF*29 else.
+template <int B>
+__device__ __forceinline__ void leaf_block(uint32_t (&st)[8], const uint32_t* __restrict__ sh, bool q0) {
+  constexpr int BASE = (B == 0) ? 0 : 16 * B - 8;
+  constexpr int NW = (B == 8) ? 8 : 20;
+  uint32_t s[20];
+  const uint4* p4 = reinterpret_cast<const uint4*>(sh + BASE);
+#pragma unroll
+  for (int i = 0; i < NW / 4; i++) {
+    const uint4 v = p4[i];
+    s[4 * i] = v.x; s[4 * i + 1] = v.y; s[4 * i + 2] = v.z; s[4 * i + 3] = v.w;
+  }
+  uint32_t w[16];
+#pragma unroll
+  for (int wi = 0; wi < 16; wi++) {
+    const int p = 64 * B + 4 * wi;
+    uint32_t x;
+    if (B == 0 && wi < 8) {
+      if (q0) {
+        if (wi == 0) x = perm(0u, s[0], 0x0C000102u);
+        else if (wi < 7) x = perm(s[wi - 1], s[wi], 0x07000102u);
+        else x = perm(s[6], s[7], 0x07000C0Cu) | perm(0u, s[0], 0x0C0C0001u);
+      } else {
+        if (wi == 0) x = 0x00FFFFFFu;
+        else if (wi < 7) x = 0xFFFFFFFFu;
+        else x = 0xFFFF0000u | perm(0u, s[0], 0x0C0C0001u);
+      }
+    } else if (p <= 536) {
+      const int a = (p - 32) / 4 - BASE;  // share dword holding bytes q, q+1 (q = p - 30)
+      x = perm(s[a], s[a + 1], 0x06070001u);
+    } else if (p == 540) {
+      x = perm(s[7], 0x80u, 0x0607000Cu);
+    } else if (p == 572) {
+      x = 542u * 8u;
+    } else {
+      x = 0u;
+    }
+    w[wi] = x;
+  }
+  sha256_compress(st, w);
+}
+
+// Namespace order: is ns(a) < ns(b)? (29-byte lexicographic compare of share prefixes)
+__device__ __forceinline__ bool ns_less(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b) {
+  const uint4* pa = reinterpret_cast<const uint4*>(a);
+  const uint4* pb = reinterpret_cast<const uint4*>(b);
+  uint32_t x[8], y[8];
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    const uint4 u = pa[i], v = pb[i];
+    x[4 * i] = u.x; x[4 * i + 1] = u.y; x[4 * i + 2] = u.z; x[4 * i + 3] = u.w;
+    y[4 * i] = v.x; y[4 * i + 1] = v.y; y[4 * i + 2] = v.z; y[4 * i + 3] = v.w;
+  }
+  int res = 0;  // -1 a<b, 1 a>b
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint32_t xa = bswap32(x[i]), yb = bswap32(y[i]);
+    if (i == 7) { xa &= 0xFF000000u; yb &= 0xFF000000u; }
+    if (res == 0 && xa != yb) res = xa < yb ? -1 : 1;
+  }
+  return res < 0;
+}
+
+// grid: x = cell block (256 cells), y = square. Writes leaf nodes [sq][W*W][24].
+template <bool ORDER>
+__global__ __launch_bounds__(256) void k_leaf(const uint8_t* __restrict__ eds, uint32_t k, uint32_t* __restrict__ leaves,
+                                              int32_t* __restrict__ bad_axis) {
+  const uint32_t W = 2 * k;
+  const uint32_t cell = blockIdx.x * 256u + threadIdx.x;
+  if (cell >= W * W) return;
+  const uint32_t r = cell / W, c = cell % W;
+  const uint64_t sq_eds = (uint64_t)W * W * kShare;
+  const uint32_t* sh = reinterpret_cast<const uint32_t*>(eds + blockIdx.y * sq_eds + (uint64_t)cell * kShare);
+  const bool q0 = (r < k) && (c < k);
+  if (ORDER && q0) {
+    if (c > 0 && ns_less(sh, sh - kShare / 4)) atomicMin(bad_axis + blockIdx.y, (int32_t)r);
+    if (r > 0 && ns_less(sh, sh - (uint64_t)W * kShare / 4)) atomicMin(bad_axis + blockIdx.y, (int32_t)(W + c));
+  }
+  uint32_t st[8];
+  sha256_init(st);
+  leaf_block<0>(st, sh, q0);
+  leaf_block<1>(st, sh, q0);
+  leaf_block<2>(st, sh, q0);
+  leaf_block<3>(st, sh, q0);
+  leaf_block<4>(st, sh, q0);
+  leaf_block<5>(st, sh, q0);
+  leaf_block<6>(st, sh, q0);
+  leaf_block<7>(st, sh, q0);
+  leaf_block<8>(st, sh, q0);
+  uint32_t nd[kNodeWords];
+  if (q0) {
+    const uint4* p4 = reinterpret_cast<const uint4*>(sh);
+    uint32_t s[8];
+    const uint4 v0 = p4[0], v1 = p4[1];
+    s[0] = v0.x; s[1] = v0.y; s[2] = v0.z; s[3] = v0.w; s[4] = v1.x; s[5] = v1.y; s[6] = v1.z; s[7] = v1.w;
+#pragma unroll
+    for (int i = 0; i < 7; i++) nd[i] = s[i];
+    nd[7] = (s[7] & 0xFFu) | (s[0] << 8);
+#pragma unroll
+    for (int i = 0; i < 6; i++) nd[8 + i] = __builtin_amdgcn_alignbyte(s[i + 1], s[i], 3);
+    nd[14] = (s[6] >> 24) | ((s[7] & 0xFFu) << 8);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 14; i++) nd[i] = 0xFFFFFFFFu;
+    nd[14] = 0xFFFFu;
+  }
+  put_digest(nd, st);
+  store_node(leaves + ((uint64_t)blockIdx.y * W * W + cell) * kNodeWords, nd);
+}
+
+// ---------------------------------------------------------------- inner nodes
+
+// HashNode(L, R): message 0x01 || L(90) || R(90) = 181 B -> 3 blocks.
+// minNs = L.min; maxNs = (R.min == 0xFF*29) ? L.max : R.max  (IgnoreMaxNamespace).
+__device__ __forceinline__ void hash_node(const uint32_t (&L)[kNodeWords], const uint32_t (&R)[kNodeWords],
+                                          uint32_t (&out)[kNodeWords]) {
+  uint32_t st[8];
+  sha256_init(st);
+#pragma unroll
+  for (int b = 0; b < 3; b++) {
+    uint32_t w[16];
+#pragma unroll
+    for (int wi = 0; wi < 16; wi++) {
+      const int q = 16 * b + wi;
+      uint32_t x;
+      if (q == 0) x = perm(1u, L[0], 0x04000102u);
+      else if (q <= 21) x = perm(L[q - 1], L[q], 0x07000102u);
+      else if (q == 22) x = perm(L[21], L[22], 0x0700010Cu) | (R[0] & 0xFFu);
+      else if (q <= 44) x = perm(R[q - 23], R[q - 22], 0x05060700u);
+      else if (q == 45) x = perm(R[22], 0x80u, 0x05000C0Cu);
+      else if (q == 47) x = 181u * 8u;
+      else x = 0u;
+      w[wi] = x;
+    }
+    sha256_compress(st, w);
+  }
+  bool rpar = (R[7] & 0xFFu) == 0xFFu;
+#pragma unroll
+  for (int i = 0; i < 7; i++) rpar = rpar && (R[i] == 0xFFFFFFFFu);
+  // out: min from L (bytes 0..28), max from L or R (bytes 29..57)
+#pragma unroll
+  for (int i = 0; i < 7; i++) out[i] = L[i];
+  const uint32_t X7 = rpar ? L[7] : R[7];
+  out[7] = (L[7] & 0xFFu) | (X7 & 0xFFFFFF00u);
+#pragma unroll
+  for (int i = 8; i < 14; i++) out[i] = rpar ? L[i] : R[i];
+  out[14] = (rpar ? L[14] : R[14]) & 0xFFFFu;
+  put_digest(out, st);
+}
+
+// One tree level for all trees. Input addressing:
+//   FROM_LEAVES: tree t < W is row t (children leaves (t, 2j), (t, 2j+1));
+//                tree t >= W is column t-W (children (2j, c), (2j+1, c)).
+//   otherwise  : in[sq][t][2j], in[sq][t][2j+1] with `nin` nodes per tree.
+template <bool FROM_LEAVES>
+__global__ __launch_bounds__(256) void k_level(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint32_t W,
+                                               uint32_t nin, uint32_t trees) {
+  const uint32_t nout = nin / 2;
+  const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
+  if (idx >= trees * nout) return;
+  const uint32_t t = idx / nout, j = idx % nout;
+  uint64_t li, ri;
+  if (FROM_LEAVES) {
+    const uint64_t sq = (uint64_t)blockIdx.y * W * W;
+    if (t < W) { li = sq + (uint64_t)t * W + 2 * j; ri = li + 1; }
+    else { li = sq + (uint64_t)(2 * j) * W + (t - W); ri = li + W; }
+  } else {
+    const uint64_t sq = (uint64_t)blockIdx.y * trees * nin;
+    li = sq + (uint64_t)t * nin + 2 * j;
+    ri = li + 1;
+  }
+  uint32_t L[kNodeWords], R[kNodeWords], o[kNodeWords];
+  load_node(in + li * kNodeWords, L);
+  load_node(in + ri * kNodeWords, R);
+  hash_node(L, R, o);
+  store_node(out + ((uint64_t)blockIdx.y * trees * nout + idx) * kNodeWords, o);
+}
+
+// Last <= 64 nodes of every tree: one 64-lane workgroup per tree (grid x = tree, y = square).
+// Odd counts carry the last node up unchanged (nmt / RFC-6962 split at the largest
+// power of two below n). Writes the root record to roots[sq][t].
+template <bool FROM_LEAVES>
+__global__ __launch_bounds__(64) void k_top(const uint32_t* __restrict__ in, uint32_t* __restrict__ roots, uint32_t W,
+                                            uint32_t nin, uint32_t trees) {
+  __shared__ __attribute__((aligned(16))) uint32_t s[64 * kNodeWords];
+  const uint32_t t = blockIdx.x, lane = threadIdx.x;
+  if (lane < nin) {
+    uint64_t li;
+    if (FROM_LEAVES) {
+      const uint64_t sq = (uint64_t)blockIdx.y * W * W;
+      li = (t < W) ? sq + (uint64_t)t * W + lane : sq + (uint64_t)lane * W + (t - W);
+    } else {
+      li = (uint64_t)blockIdx.y * trees * nin + (uint64_t)t * nin + lane;
+    }
+    const uint4* src = reinterpret_cast<const uint4*>(in + li * kNodeWords);
+    uint4* dst = reinterpret_cast<uint4*>(s + lane * kNodeWords);
+#pragma unroll
+    for (int i = 0; i < 6; i++) dst[i] = src[i];
+  }
+  __syncthreads();
+  uint32_t n = nin;
+  while (n > 1) {
+    const uint32_t half = n / 2;
+    uint32_t o[kNodeWords];
+    if (lane < half) {
+      uint32_t L[kNodeWords], R[kNodeWords];
+      load_node(s + (2 * lane) * kNodeWords, L);
+      load_node(s + (2 * lane + 1) * kNodeWords, R);
+      hash_node(L, R, o);
+    }
+    __syncthreads();
+    if (lane < half) store_node(s + lane * kNodeWords, o);
+    if ((n & 1) && lane == 0) {
+      uint4* dst = reinterpret_cast<uint4*>(s + half * kNodeWords);
+      const uint4* src = reinterpret_cast<const uint4*>(s + (n - 1) * kNodeWords);
+      for (int i = 0; i < 6; i++) dst[i] = src[i];
+    }
+    __syncthreads();
+    n = half + (n & 1);
+  }
+  if (lane < kNodeWords) roots[((uint64_t)blockIdx.y * trees + t) * kNodeWords + lane] = s[lane];
+}
+
+// ------------------------------------------------------------------ RFC-6962
+
+// leafHash = SHA256(0x00 || item) for a 90-byte item (2 blocks).
+__device__ __forceinline__ void rfc_leaf90(const uint32_t (&R)[kNodeWords], uint32_t (&st)[8]) {
+  sha256_init(st);
+#pragma unroll
+  for (int b = 0; b < 2; b++) {
+    uint32_t w[16];
+#pragma unroll
+    for (int wi = 0; wi < 16; wi++) {
+      const int q = 16 * b + wi;
+      uint32_t x;
+      if (q == 0) x = perm(0u, R[0], 0x0C000102u);
+      else if (q <= 21) x = perm(R[q - 1], R[q], 0x07000102u);
+      else if (q == 22) x = perm(R[21], R[22], 0x0700010Cu) | 0x80u;
+      else if (q == 31) x = 91u * 8u;
+      else x = 0u;
+      w[wi] = x;
+    }
+    sha256_compress(st, w);
+  }
+}
+
+// innerHash = SHA256(0x01 || l(32) || r(32)) (2 blocks).
+__device__ __forceinline__ void rfc_inner(const uint32_t* l, const uint32_t* r, uint32_t (&st)[8]) {
+  uint32_t w[16];
+  w[0] = 0x01000000u | (l[0] >> 8);
+#pragma unroll
+  for (int i = 1; i < 8; i++) w[i] = __builtin_amdgcn_alignbit(l[i - 1], l[i], 8);
+  w[8] = __builtin_amdgcn_alignbit(l[7], r[0], 8);
+#pragma unroll
+  for (int i = 9; i < 16; i++) w[i] = __builtin_amdgcn_alignbit(r[i - 9], r[i - 8], 8);
+  sha256_init(st);
+  sha256_compress(st, w);
+  uint32_t w2[16];
+  w2[0] = (r[7] << 24) | 0x00800000u;
+#pragma unroll
+  for (int i = 1; i < 15; i++) w2[i] = 0;
+  w2[15] = 65u * 8u;
+  sha256_compress(st, w2);
+}
+
+// SHA256 of the empty string (RFC-6962 empty tree).
+__device__ __forceinline__ void sha_empty(uint32_t (&st)[8]) {
+  uint32_t w[16];
+  w[0] = 0x80000000u;
+#pragma unroll
+  for (int i = 1; i < 16; i++) w[i] = 0;
+  sha256_init(st);
+  sha256_compress(st, w);
+}
+
+// One workgroup per item list: items[g][n] 96-byte records -> 32-byte root (BE words in
+// out[g*8..]). Also packs the first n items into 90-byte outputs (row/col roots) if given.
+__global__ __launch_bounds__(256) void k_merkle(const uint32_t* __restrict__ items, uint32_t n, uint8_t* __restrict__ dah,
+                                                uint8_t* __restrict__ row_out, uint8_t* __restrict__ col_out,
+                                                const int32_t* __restrict__ bad_axis, int32_t* __restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t hs[];  // n * 8 words
+  const uint32_t g = blockIdx.x;
+  const uint32_t* it = items + (uint64_t)g * n * kNodeWords;
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    uint32_t R[kNodeWords], st[8];
+    load_node(it + (uint64_t)i * kNodeWords, R);
+    rfc_leaf90(R, st);
+#pragma unroll
+    for (int j = 0; j < 8; j++) hs[i * 8 + j] = st[j];
+  }
+  // pack 90-byte roots (first half rows, second half columns)
+  if (row_out) {
+    const uint32_t half = n / 2;
+    for (uint32_t b = threadIdx.x; b < n * kNode; b += blockDim.x) {
+      const uint32_t i = b / kNode, o = b % kNode;
+      const uint8_t v = reinterpret_cast<const uint8_t*>(it + (uint64_t)i * kNodeWords)[o];
+      if (i < half) row_out[((uint64_t)g * half + i) * kNode + o] = v;
+      else col_out[((uint64_t)g * half + (i - half)) * kNode + o] = v;
+    }
+  }
+  __syncthreads();
+  uint32_t cnt = n;
+  while (cnt > 1) {
+    const uint32_t half = cnt / 2;
+    uint32_t st[8];
+    for (uint32_t base = 0; base < half; base += blockDim.x) {
+      const uint32_t i = base + threadIdx.x;
+      if (i < half) rfc_inner(hs + (2 * i) * 8, hs + (2 * i + 1) * 8, st);
+      __syncthreads();
+      if (i < half) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) hs[i * 8 + j] = st[j];
+      }
+      __syncthreads();
+    }
+    if (cnt & 1) {
+      if (threadIdx.x < 8) hs[half * 8 + threadIdx.x] = hs[(cnt - 1) * 8 + threadIdx.x];
+      __syncthreads();
+    }
+    cnt = half + (cnt & 1);
+  }
+  if (threadIdx.x == 0) {
+    uint32_t st[8];
+    if (n == 0) sha_empty(st);
+    else
+      for (int j = 0; j < 8; j++) st[j] = hs[j];
+    for (int j = 0; j < 8; j++) {
+      dah[g * 32 + 4 * j] = (uint8_t)(st[j] >> 24);
+      dah[g * 32 + 4 * j + 1] = (uint8_t)(st[j] >> 16);
+      dah[g * 32 + 4 * j + 2] = (uint8_t)(st[j] >> 8);
+      dah[g * 32 + 4 * j + 3] = (uint8_t)st[j];
+    }
+    if (status) status[g] = (bad_axis && bad_axis[g] != INT_MAX) ? CEL_EORDER : CEL_OK;
+  }
+}
+
+__global__ void k_fill_i32(int32_t* p, uint32_t n, int32_t v) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+// ----------------------------------------------------------------- launchers
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// Workspace: leaves [nsq][W*W] nodes | ping [nsq][2W][W/2] | pong [nsq][2W][W/4] |
+//            roots [nsq][2W] nodes | bad_axis [nsq] int32
+size_t nmt_workspace_size(uint32_t k, uint32_t nsq) {
+  const size_t W = 2 * (size_t)k, nb = kNodeWords * 4;
+  return align256(nsq * W * W * nb) + align256(nsq * 2 * W * (W / 2 + 1) * nb) +
+         align256(nsq * 2 * W * (W / 4 + 1) * nb) + align256(nsq * 2 * W * nb) + align256(nsq * 4 + 4);
+}
+
+hipError_t launch_commit(const uint8_t* eds, uint32_t k, uint32_t nsq, uint8_t* row_roots, uint8_t* col_roots,
+                         uint8_t* dah, int32_t* status, void* work, bool order_check, hipStream_t s) {
+  const uint32_t W = 2 * k;
+  const size_t nb = kNodeWords * 4;
+  uint8_t* base = static_cast<uint8_t*>(work);
+  uint32_t* leaves = reinterpret_cast<uint32_t*>(base);
+  base += align256((size_t)nsq * W * W * nb);
+  uint32_t* ping = reinterpret_cast<uint32_t*>(base);
+  base += align256((size_t)nsq * 2 * W * (W / 2 + 1) * nb);
+  uint32_t* pong = reinterpret_cast<uint32_t*>(base);
+  base += align256((size_t)nsq * 2 * W * (W / 4 + 1) * nb);
+  uint32_t* roots = reinterpret_cast<uint32_t*>(base);
+  base += align256((size_t)nsq * 2 * W * nb);
+  int32_t* bad = reinterpret_cast<int32_t*>(base);
+
+  hipLaunchKernelGGL(k_fill_i32, dim3((nsq + 255) / 256), dim3(256), 0, s, bad, nsq, INT_MAX);
+  dim3 gl((W * W + 255) / 256, nsq);
+  if (order_check) hipLaunchKernelGGL(k_leaf<true>, gl, dim3(256), 0, s, eds, k, leaves, bad);
+  else hipLaunchKernelGGL(k_leaf<false>, gl, dim3(256), 0, s, eds, k, leaves, bad);
+
+  const uint32_t trees = 2 * W;
+  if (W <= 64) {
+    hipLaunchKernelGGL(k_top<true>, dim3(trees, nsq), dim3(64), 0, s, leaves, roots, W, W, trees);
+  } else {
+    uint32_t nin = W;
+    const uint32_t* src = leaves;
+    uint32_t* dst = ping;
+    bool first = true;
+    while (nin > 64) {
+      const uint32_t nout = nin / 2;
+      dim3 g((trees * nout + 255) / 256, nsq);
+      if (first) hipLaunchKernelGGL(k_level<true>, g, dim3(256), 0, s, src, dst, W, nin, trees);
+      else hipLaunchKernelGGL(k_level<false>, g, dim3(256), 0, s, src, dst, W, nin, trees);
+      first = false;
+      src = dst;
+      dst = (dst == ping) ? pong : ping;
+      nin = nout;
+    }
+    hipLaunchKernelGGL(k_top<false>, dim3(trees, nsq), dim3(64), 0, s, src, roots, W, nin, trees);
+  }
+  const size_t lds = (size_t)trees * 8 * 4;
+  hipLaunchKernelGGL(k_merkle, dim3(nsq), dim3(256), lds, s, roots, trees, dah, row_roots, col_roots, bad, status);
+  return hipGetLastError();
+}
+
+// Plain NMT over arbitrary leaves (k_leaf assumes 512-byte EDS cells, so leaves are
+// hashed by a generic lane-per-leaf kernel over a byte message).
+__device__ void sha_bytes(const uint8_t* __restrict__ a, uint32_t la, const uint8_t* __restrict__ b, uint32_t lb,
+                          uint8_t pre, uint32_t (&st)[8]) {
+  // message = pre || a || b; processed byte-wise (generic path, small inputs only)
+  const uint64_t total = 1ull + la + lb;
+  sha256_init(st);
+  uint32_t w[16];
+  uint64_t pos = 0;
+  const uint64_t padded = ((total + 8) / 64 + 1) * 64;
+  for (uint64_t blk = 0; blk < padded; blk += 64) {
+    for (int wi = 0; wi < 16; wi++) {
+      uint32_t x = 0;
+      for (int j = 0; j < 4; j++) {
+        const uint64_t p = blk + 4 * wi + j;
+        uint32_t v;
+        if (p == 0) v = pre;
+        else if (p < 1 + la) v = a[p - 1];
+        else if (p < total) v = b[p - 1 - la];
+        else if (p == total) v = 0x80;
+        else if (p >= padded - 8) v = (uint32_t)(((total * 8) >> (8 * (padded - 1 - p))) & 0xFF);
+        else v = 0;
+        x = (x << 8) | v;
+      }
+      w[wi] = x;
+    }
+    sha256_compress(st, w);
+    pos += 64;
+  }
+  (void)pos;
+}
+
+__global__ __launch_bounds__(256) void k_generic_leaf(const uint8_t* __restrict__ leaves, uint32_t n, uint32_t len,
+                                                      uint32_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t* lf = leaves + (uint64_t)i * len;
+  uint32_t st[8];
+  sha_bytes(lf, len, nullptr, 0, 0x00, st);
+  uint32_t nd[kNodeWords];
+  uint8_t* nb = reinterpret_cast<uint8_t*>(nd);
+  for (int j = 0; j < 29; j++) { nb[j] = lf[j]; nb[29 + j] = lf[j]; }
+  nb[58] = nb[59] = 0;
+  nd[14] &= 0xFFFFu;
+  put_digest(nd, st);
+  store_node(out + (uint64_t)i * kNodeWords, nd);
+}
+
+// Erasured axis: cells (2k x 512 B) with the wrapper's namespace rule.
+__global__ __launch_bounds__(256) void k_axis_leaf(const uint8_t* __restrict__ cells, uint32_t k, uint32_t axis,
+                                                   uint32_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= 2 * k) return;
+  const uint32_t* sh = reinterpret_cast<const uint32_t*>(cells + (uint64_t)i * kShare);
+  const bool q0 = (i < k) && (axis < k);
+  uint32_t st[8];
+  sha256_init(st);
+  leaf_block<0>(st, sh, q0);
+  leaf_block<1>(st, sh, q0);
+  leaf_block<2>(st, sh, q0);
+  leaf_block<3>(st, sh, q0);
+  leaf_block<4>(st, sh, q0);
+  leaf_block<5>(st, sh, q0);
+  leaf_block<6>(st, sh, q0);
+  leaf_block<7>(st, sh, q0);
+  leaf_block<8>(st, sh, q0);
+  uint32_t nd[kNodeWords];
+  if (q0) {
+    uint32_t s[8];
+    for (int j = 0; j < 8; j++) s[j] = sh[j];
+    for (int j = 0; j < 7; j++) nd[j] = s[j];
+    nd[7] = (s[7] & 0xFFu) | (s[0] << 8);
+    for (int j = 0; j < 6; j++) nd[8 + j] = __builtin_amdgcn_alignbyte(s[j + 1], s[j], 3);
+    nd[14] = (s[6] >> 24) | ((s[7] & 0xFFu) << 8);
+  } else {
+    for (int j = 0; j < 14; j++) nd[j] = 0xFFFFFFFFu;
+    nd[14] = 0xFFFFu;
+  }
+  put_digest(nd, st);
+  store_node(out + (uint64_t)i * kNodeWords, nd);
+}
+
+// Reduce n nodes (one tree) to a root with repeated k_level-like passes, then pack.
+__global__ __launch_bounds__(256) void k_reduce_pass(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                     uint32_t n) {
+  const uint32_t half = n / 2;
+  const uint32_t j = blockIdx.x * 256u + threadIdx.x;
+  if (j < half) {
+    uint32_t L[kNodeWords], R[kNodeWords], o[kNodeWords];
+    load_node(in + (uint64_t)(2 * j) * kNodeWords, L);
+    load_node(in + (uint64_t)(2 * j + 1) * kNodeWords, R);
+    hash_node(L, R, o);
+    store_node(out + (uint64_t)j * kNodeWords, o);
+  } else if ((n & 1) && j == half) {
+    uint32_t x[kNodeWords];
+    load_node(in + (uint64_t)(n - 1) * kNodeWords, x);
+    store_node(out + (uint64_t)half * kNodeWords, x);
+  }
+}
+
+__global__ void k_pack_root(const uint32_t* __restrict__ node, uint32_t n, uint8_t* __restrict__ out) {
+  const uint32_t i = threadIdx.x;
+  if (i >= kNode) return;
+  if (n == 0) {  // empty tree: 0*58 || SHA256("")
+    if (i < 58) out[i] = 0;
+    if (i == 0) {
+      uint32_t st[8];
+      sha_empty(st);
+      for (int j = 0; j < 32; j++) out[58 + j] = (uint8_t)(st[j / 4] >> (24 - 8 * (j % 4)));
+    }
+    return;
+  }
+  out[i] = reinterpret_cast<const uint8_t*>(node)[i];
+}
+
+static hipError_t reduce_tree(uint32_t* a, uint32_t* b, uint32_t n, uint8_t* root, hipStream_t s) {
+  uint32_t* src = a;
+  uint32_t* dst = b;
+  while (n > 1) {
+    const uint32_t nout = n / 2 + (n & 1);
+    hipLaunchKernelGGL(k_reduce_pass, dim3((nout + 255) / 256), dim3(256), 0, s, src, dst, n);
+    uint32_t* t = src;
+    src = dst;
+    dst = t;
+    n = nout;
+  }
+  hipLaunchKernelGGL(k_pack_root, dim3(1), dim3(128), 0, s, src, n, root);
+  return hipGetLastError();
+}
+
+size_t axis_root_workspace_size(uint32_t k) { return 2 * align256((size_t)2 * k * kNodeWords * 4); }
+
+hipError_t launch_axis_root(const uint8_t* cells, uint32_t k, uint32_t axis, uint8_t* root, void* work,
+                            hipStream_t s) {
+  uint32_t* a = static_cast<uint32_t*>(work);
+  uint32_t* b = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(work) + align256((size_t)2 * k * kNodeWords * 4));
+  hipLaunchKernelGGL(k_axis_leaf, dim3((2 * k + 255) / 256), dim3(256), 0, s, cells, k, axis, a);
+  return reduce_tree(a, b, 2 * k, root, s);
+}
+
+size_t nmt_root_workspace_size(uint32_t n) { return 2 * align256((size_t)(n ? n : 1) * kNodeWords * 4); }
+
+hipError_t launch_nmt_root(const uint8_t* leaves, uint32_t n, uint32_t len, uint8_t* root, void* work,
+                           hipStream_t s) {
+  uint32_t* a = static_cast<uint32_t*>(work);
+  uint32_t* b = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(work) + align256((size_t)(n ? n : 1) * kNodeWords * 4));
+  if (n) hipLaunchKernelGGL(k_generic_leaf, dim3((n + 255) / 256), dim3(256), 0, s, leaves, n, len, a);
+  return reduce_tree(a, b, n, root, s);
+}
+
+// Roots of `naxes` erasured axes held densely as cells[a][2k][512]; axis_idx[a] is the
+// row/column index that decides the Q0 namespace rule. roots: [naxes] 96-byte records.
+__global__ __launch_bounds__(256) void k_axes_leaf(const uint8_t* __restrict__ cells, uint32_t k,
+                                                   const int32_t* __restrict__ axis_idx, uint32_t naxes,
+                                                   uint32_t* __restrict__ out) {
+  const uint32_t W = 2 * k;
+  const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+  if (g >= naxes * W) return;
+  const uint32_t a = g / W, i = g % W;
+  const uint32_t* sh = reinterpret_cast<const uint32_t*>(cells + (uint64_t)g * kShare);
+  const bool q0 = (i < k) && ((uint32_t)axis_idx[a] < k);
+  uint32_t st[8];
+  sha256_init(st);
+  leaf_block<0>(st, sh, q0);
+  leaf_block<1>(st, sh, q0);
+  leaf_block<2>(st, sh, q0);
+  leaf_block<3>(st, sh, q0);
+  leaf_block<4>(st, sh, q0);
+  leaf_block<5>(st, sh, q0);
+  leaf_block<6>(st, sh, q0);
+  leaf_block<7>(st, sh, q0);
+  leaf_block<8>(st, sh, q0);
+  uint32_t nd[kNodeWords];
+  if (q0) {
+    uint32_t s[8];
+    for (int j = 0; j < 8; j++) s[j] = sh[j];
+    for (int j = 0; j < 7; j++) nd[j] = s[j];
+    nd[7] = (s[7] & 0xFFu) | (s[0] << 8);
+    for (int j = 0; j < 6; j++) nd[8 + j] = __builtin_amdgcn_alignbyte(s[j + 1], s[j], 3);
+    nd[14] = (s[6] >> 24) | ((s[7] & 0xFFu) << 8);
+  } else {
+    for (int j = 0; j < 14; j++) nd[j] = 0xFFFFFFFFu;
+    nd[14] = 0xFFFFu;
+  }
+  put_digest(nd, st);
+  store_node(out + (uint64_t)g * kNodeWords, nd);
+}
+
+size_t axes_roots_workspace_size(uint32_t k, uint32_t naxes) {
+  const size_t W = 2 * (size_t)k, nb = kNodeWords * 4;
+  return align256(naxes * W * nb) + align256(naxes * (W / 2 + 1) * nb) + align256(naxes * (W / 4 + 1) * nb);
+}
+
+hipError_t launch_axes_roots(const uint8_t* cells, uint32_t k, const int32_t* axis_idx, uint32_t naxes,
+                             uint32_t* roots, void* work, hipStream_t s) {
+  const uint32_t W = 2 * k;
+  const size_t nb = kNodeWords * 4;
+  uint8_t* base = static_cast<uint8_t*>(work);
+  uint32_t* leaves = reinterpret_cast<uint32_t*>(base);
+  base += align256((size_t)naxes * W * nb);
+  uint32_t* ping = reinterpret_cast<uint32_t*>(base);
+  base += align256((size_t)naxes * (W / 2 + 1) * nb);
+  uint32_t* pong = reinterpret_cast<uint32_t*>(base);
+  hipLaunchKernelGGL(k_axes_leaf, dim3((naxes * W + 255) / 256), dim3(256), 0, s, cells, k, axis_idx, naxes, leaves);
+  uint32_t nin = W;
+  const uint32_t* src = leaves;
+  uint32_t* dst = ping;
+  while (nin > 64) {
+    const uint32_t nout = nin / 2;
+    hipLaunchKernelGGL(k_level<false>, dim3((naxes * nout + 255) / 256, 1), dim3(256), 0, s, src, dst, W, nin, naxes);
+    src = dst;
+    dst = (dst == ping) ? pong : ping;
+    nin = nout;
+  }
+  hipLaunchKernelGGL(k_top<false>, dim3(naxes, 1), dim3(64), 0, s, src, roots, W, nin, naxes);
+  return hipGetLastError();
+}
+
+size_t merkle_workspace_size(uint32_t n) { return align256((size_t)(n ? n : 1) * kNodeWords * 4); }
+
+__global__ void k_pad_items(const uint8_t* __restrict__ items, uint32_t n, uint32_t len, uint32_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t* o = reinterpret_cast<uint8_t*>(out + (uint64_t)i * kNodeWords);
+  for (uint32_t j = 0; j < kNodeWords * 4; j++) o[j] = j < len ? items[(uint64_t)i * len + j] : 0;
+}
+
+hipError_t launch_merkle_root(const uint8_t* items, uint32_t n, uint32_t item_len, uint8_t* out, void* work,
+                              hipStream_t s) {
+  if (item_len != kNode) return hipErrorInvalidValue;  // DAH items are NMT roots
+  uint32_t* pad = static_cast<uint32_t*>(work);
+  if (n) hipLaunchKernelGGL(k_pad_items, dim3((n + 255) / 256), dim3(256), 0, s, items, n, item_len, pad);
+  const size_t lds = (size_t)(n ? n : 1) * 8 * 4;
+  if (lds > 64 * 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_merkle, dim3(1), dim3(256), lds, s, pad, n, out, nullptr, nullptr, nullptr, nullptr);
+  return hipGetLastError();
+}
+
+}  // namespace cel

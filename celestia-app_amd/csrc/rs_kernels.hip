@@ -1,0 +1,546 @@
+// Leopard Reed-Solomon on gfx950: encode (GF(2^8), GF(2^16)) and erasure decode.
+//
+// Replaces klauspost/reedsolomon v1.12.1 leopard8.go / leopard.go Encode and
+// Reconstruct as driven by rsmt2d v0.14.0 LeoRSCodec (DefaultCodec,
+// pkg/appconsts/global_consts.go:92). Algorithm: SURVEY.md Appendix A.2/A.3,
+// written here in radix-2 form:
+//   IFFT over the data coset (offset m): for D = 1, 2, .., m/2, every pair
+//     (a, a+D) with base = a & ~(2D-1):  y ^= x; x ^= y * exp(skew[m-1 + base + D])
+//   FFT over the parity coset (offset 0): for D = m/2, .., 1:
+//     x ^= y * exp(skew[base + D - 1]); y ^= x
+// A skew value equal to the field modulus means "multiply by zero" (the xor-only
+// butterfly of the reference).
+//
+// GF(2^8) encode keeps one 32-bit column of every shard of an axis in VGPRs
+// (k <= 128 dwords per lane): the whole transform is lane-local, with no LDS and
+// no barriers. A multiply by the (wave-uniform) twiddle c splits each byte into
+// 3+3+2 bits and looks each piece up with one v_perm_b32 in an 8/8/4-entry
+// product table held in SGPRs: 10-12 VALU ops per 4 bytes.
+//
+// GF(2^16) (k >= 256) and the decoder stage a 64-byte chunk of every shard of
+// an axis in LDS (k <= 2048 -> <= 128 KiB) and run radix-2 layers with a
+// barrier per layer.
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "cel_internal.hpp"
+#include "leopard_field.hpp"
+
+namespace cel {
+
+// ------------------------------------------------------------------ tables
+
+// Product tables for the v_perm multiply: for constant c = exp(lm):
+//   T0[n] = c*n (n<8), T1[n] = c*(n<<3) (n<8), T2[n] = c*(n<<6) (n<4)
+// packed as {T0[0..3], T0[4..7], T1[0..3], T1[4..7], T2[0..3], 0, 0, 0}.
+// lm == 255 (the "zero twiddle" sentinel) gives all-zero tables.
+static void perm_table8(const LeoField& f, uint32_t lm, uint32_t out[8]) {
+  for (int i = 0; i < 8; i++) out[i] = 0;
+  if (lm == f.mod) return;
+  auto mul = [&](uint32_t a) { return f.mul_log(a, lm) & 0xFF; };
+  for (uint32_t n = 0; n < 8; n++) {
+    out[n >> 2] |= mul(n) << (8 * (n & 3));
+    out[2 + (n >> 2)] |= mul(n << 3) << (8 * (n & 3));
+  }
+  for (uint32_t n = 0; n < 4; n++) out[4] |= mul(n << 6) << (8 * n);
+}
+
+hipError_t upload_tables(DeviceTables* t) {
+  const LeoField& f8 = leo_gf8();
+  const LeoField& f16 = leo_gf16();
+  std::vector<uint32_t> tw(255 * 8), mul8(256 * 8);
+  for (uint32_t i = 0; i < 255; i++) perm_table8(f8, f8.skew[i], &tw[i * 8]);
+  for (uint32_t lm = 0; lm < 256; lm++) perm_table8(f8, lm == 255 ? 0 : lm, &mul8[lm * 8]);
+  // mul8[255] is "multiply by exp(255) = 1" (a real log value, not the skew sentinel)
+  {
+    uint32_t one[8];
+    for (int i = 0; i < 8; i++) one[i] = 0;
+    for (uint32_t n = 0; n < 8; n++) {
+      one[n >> 2] |= n << (8 * (n & 3));
+      one[2 + (n >> 2)] |= (n << 3) << (8 * (n & 3));
+    }
+    for (uint32_t n = 0; n < 4; n++) one[4] |= (n << 6) << (8 * n);
+    for (int i = 0; i < 8; i++) mul8[255 * 8 + i] = one[i];
+  }
+  hipError_t e;
+  if ((e = hipMalloc(&t->tw8, tw.size() * 4)) != hipSuccess) return e;
+  if ((e = hipMalloc(&t->mul8, mul8.size() * 4)) != hipSuccess) return e;
+  if ((e = hipMalloc(&t->exp16, 65536 * 2)) != hipSuccess) return e;
+  if ((e = hipMalloc(&t->log16, 65536 * 2)) != hipSuccess) return e;
+  if ((e = hipMalloc(&t->skew16, 65535 * 2)) != hipSuccess) return e;
+  if ((e = hipMemcpy(t->tw8, tw.data(), tw.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return e;
+  if ((e = hipMemcpy(t->mul8, mul8.data(), mul8.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return e;
+  if ((e = hipMemcpy(t->exp16, f16.exp.data(), 65536 * 2, hipMemcpyHostToDevice)) != hipSuccess) return e;
+  if ((e = hipMemcpy(t->log16, f16.log.data(), 65536 * 2, hipMemcpyHostToDevice)) != hipSuccess) return e;
+  return hipMemcpy(t->skew16, f16.skew.data(), 65535 * 2, hipMemcpyHostToDevice);
+}
+
+void free_tables(DeviceTables* t) {
+  (void)hipFree(t->tw8);
+  (void)hipFree(t->mul8);
+  (void)hipFree(t->exp16);
+  (void)hipFree(t->log16);
+  (void)hipFree(t->skew16);
+  *t = DeviceTables{};
+}
+
+// GF(2^8) tables for the LDS kernels (exp/log, 256 entries each).
+struct Gf8Small {
+  uint8_t exp[256];
+  uint8_t log[256];
+  uint8_t skew[256];
+};
+__constant__ Gf8Small c_gf8;
+static bool g_gf8_const_ready = false;
+
+static hipError_t ensure_gf8_const() {
+  if (g_gf8_const_ready) return hipSuccess;
+  const LeoField& f = leo_gf8();
+  Gf8Small h;
+  for (int i = 0; i < 256; i++) {
+    h.exp[i] = (uint8_t)f.exp[i];
+    h.log[i] = (uint8_t)f.log[i];
+    h.skew[i] = i < 255 ? (uint8_t)f.skew[i] : 0;
+  }
+  hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_gf8), &h, sizeof(h));
+  if (e == hipSuccess) g_gf8_const_ready = true;
+  return e;
+}
+
+// ------------------------------------------------ GF(2^8) register encode
+
+struct PermTab {
+  uint32_t t0l, t0h, t1l, t1h, t2;
+};
+
+__device__ __forceinline__ PermTab load_tab(const uint32_t* __restrict__ tw, int idx) {
+  const uint32_t* p = tw + idx * 8;
+  return PermTab{p[0], p[1], p[2], p[3], p[4]};
+}
+
+// 4 parallel GF(2^8) products y*c with c given by its product tables.
+__device__ __forceinline__ uint32_t gf8_mul4(uint32_t y, const PermTab& t) {
+  const uint32_t s0 = y & 0x07070707u;
+  const uint32_t s1 = (y >> 3) & 0x07070707u;
+  const uint32_t s2 = (y >> 6) & 0x03030303u;
+  return __builtin_amdgcn_perm(t.t0h, t.t0l, s0) ^ __builtin_amdgcn_perm(t.t1h, t.t1l, s1) ^
+         __builtin_amdgcn_perm(0u, t.t2, s2);
+}
+
+template <int LOGK>
+__device__ __forceinline__ void leo_encode_regs(uint32_t (&w)[1 << LOGK], const uint32_t* __restrict__ tw) {
+  constexpr int M = 1 << LOGK;
+  // IFFT over the data coset.
+#pragma unroll
+  for (int lg = 0; lg < LOGK; lg++) {
+    const int D = 1 << lg;
+#pragma unroll
+    for (int base = 0; base < M; base += 2 * D) {
+      const PermTab t = load_tab(tw, M - 1 + base + D);
+#pragma unroll
+      for (int j = 0; j < D; j++) {
+        uint32_t& x = w[base + j];
+        uint32_t& y = w[base + j + D];
+        y ^= x;
+        x ^= gf8_mul4(y, t);
+      }
+    }
+  }
+  // FFT over the parity coset.
+#pragma unroll
+  for (int lg = LOGK - 1; lg >= 0; lg--) {
+    const int D = 1 << lg;
+#pragma unroll
+    for (int base = 0; base < M; base += 2 * D) {
+      const PermTab t = load_tab(tw, base + D - 1);
+#pragma unroll
+      for (int j = 0; j < D; j++) {
+        uint32_t& x = w[base + j];
+        uint32_t& y = w[base + j + D];
+        x ^= gf8_mul4(y, t);
+        y ^= x;
+      }
+    }
+  }
+}
+
+// grid: x = axis, y = 512-byte slice of the shard, z = square. block: 128 lanes,
+// lane t owns bytes [4t, 4t+4) of the slice in every shard of the axis.
+template <int LOGK>
+__global__ __launch_bounds__(128) void k_rs_encode_gf8(RsGeom g, const uint32_t* __restrict__ tw) {
+  constexpr int M = 1 << LOGK;
+  const uint32_t off = blockIdx.y * 512u + threadIdx.x * 4u;
+  if (off >= g.len) return;
+  const uint8_t* src = g.in + (uint64_t)blockIdx.z * g.in_sq + (uint64_t)blockIdx.x * g.in_axis + off;
+  uint8_t* dst = g.out + (uint64_t)blockIdx.z * g.out_sq + (uint64_t)blockIdx.x * g.out_axis + off;
+  uint32_t w[M];
+#pragma unroll
+  for (int i = 0; i < M; i++) w[i] = *reinterpret_cast<const uint32_t*>(src + (uint64_t)i * g.in_shard);
+  if (g.dcopy) {
+    uint8_t* dc = g.dcopy + (uint64_t)blockIdx.z * g.dc_sq + (uint64_t)blockIdx.x * g.dc_axis + off;
+#pragma unroll
+    for (int i = 0; i < M; i++) *reinterpret_cast<uint32_t*>(dc + (uint64_t)i * g.dc_shard) = w[i];
+  }
+  leo_encode_regs<LOGK>(w, tw);
+#pragma unroll
+  for (int i = 0; i < M; i++) *reinterpret_cast<uint32_t*>(dst + (uint64_t)i * g.out_shard) = w[i];
+}
+
+// ------------------------------------------------- LDS transform kernels
+
+// Field ops for the LDS kernels. A "unit" is one dword of 4 GF(2^8) symbols, or
+// a GF(2^16) quad: lo-byte dword j and hi-byte dword j+8 of a 64-byte chunk.
+struct Gf8Ops {
+  static constexpr uint32_t MOD = 255;
+  static constexpr int UNITS = 16;  // dwords per 64-byte chunk
+  const uint8_t* lexp;
+  const uint8_t* llog;
+  __device__ uint32_t mul_log1(uint32_t a, uint32_t lm) const {
+    if (!a) return 0;
+    uint32_t s = llog[a] + lm;
+    s = (s + (s >> 8)) & 255u;
+    return lexp[s];
+  }
+  __device__ void muladd(uint32_t* chunk_x, const uint32_t* chunk_y, int u, uint32_t lm) const {
+    const uint32_t y = chunk_y[u];
+    uint32_t p = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) p |= mul_log1((y >> (8 * b)) & 0xFF, lm) << (8 * b);
+    chunk_x[u] ^= p;
+  }
+  __device__ void xorin(uint32_t* chunk_y, const uint32_t* chunk_x, int u) const { chunk_y[u] ^= chunk_x[u]; }
+  __device__ void scale(uint32_t* chunk, int u, uint32_t lm) const {
+    uint32_t y = chunk[u], p = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) p |= mul_log1((y >> (8 * b)) & 0xFF, lm) << (8 * b);
+    chunk[u] = p;
+  }
+};
+
+struct Gf16Ops {
+  static constexpr uint32_t MOD = 65535;
+  static constexpr int UNITS = 8;  // quads per 64-byte chunk
+  const uint16_t* __restrict__ gexp;
+  const uint16_t* __restrict__ glog;
+  __device__ uint32_t mul_log1(uint32_t a, uint32_t lm) const {
+    if (!a) return 0;
+    uint32_t s = glog[a] + lm;
+    s = (s + (s >> 16)) & 65535u;
+    return gexp[s];
+  }
+  __device__ void muladd(uint32_t* cx, const uint32_t* cy, int u, uint32_t lm) const {
+    const uint32_t lo = cy[u], hi = cy[u + 8];
+    uint32_t plo = 0, phi = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const uint32_t s = ((lo >> (8 * b)) & 0xFF) | (((hi >> (8 * b)) & 0xFF) << 8);
+      const uint32_t p = mul_log1(s, lm);
+      plo |= (p & 0xFF) << (8 * b);
+      phi |= (p >> 8) << (8 * b);
+    }
+    cx[u] ^= plo;
+    cx[u + 8] ^= phi;
+  }
+  __device__ void xorin(uint32_t* cy, const uint32_t* cx, int u) const {
+    cy[u] ^= cx[u];
+    cy[u + 8] ^= cx[u + 8];
+  }
+  __device__ void scale(uint32_t* c, int u, uint32_t lm) const {
+    const uint32_t lo = c[u], hi = c[u + 8];
+    uint32_t plo = 0, phi = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const uint32_t s = ((lo >> (8 * b)) & 0xFF) | (((hi >> (8 * b)) & 0xFF) << 8);
+      const uint32_t p = mul_log1(s, lm);
+      plo |= (p & 0xFF) << (8 * b);
+      phi |= (p >> 8) << (8 * b);
+    }
+    c[u] = plo;
+    c[u + 8] = phi;
+  }
+};
+
+// Radix-2 transform layers over `npts` chunks of 16 dwords in LDS.
+// ifft: D ascending, constant skew[off + base + D - 1]; y ^= x; x ^= y*c
+// fft:  D descending, constant skew[base + D - 1];      x ^= y*c; y ^= x
+template <class Ops, class SkewFn>
+__device__ void lds_ifft(const Ops& ops, uint32_t* lds, uint32_t npts, uint32_t off, SkewFn skew) {
+  const uint32_t items = (npts / 2) * Ops::UNITS;
+  for (uint32_t D = 1; D < npts; D <<= 1) {
+    for (uint32_t it = threadIdx.x; it < items; it += blockDim.x) {
+      const uint32_t pair = it / Ops::UNITS, u = it % Ops::UNITS;
+      const uint32_t base = (pair / D) * 2 * D, a = base + pair % D;
+      uint32_t* x = lds + a * 16;
+      uint32_t* y = lds + (a + D) * 16;
+      const uint32_t lm = skew(off + base + D - 1);
+      ops.xorin(y, x, u);
+      if (lm != Ops::MOD) ops.muladd(x, y, u, lm);
+    }
+    __syncthreads();
+  }
+}
+
+template <class Ops, class SkewFn>
+__device__ void lds_fft(const Ops& ops, uint32_t* lds, uint32_t npts, SkewFn skew) {
+  const uint32_t items = (npts / 2) * Ops::UNITS;
+  for (uint32_t D = npts >> 1; D >= 1; D >>= 1) {
+    for (uint32_t it = threadIdx.x; it < items; it += blockDim.x) {
+      const uint32_t pair = it / Ops::UNITS, u = it % Ops::UNITS;
+      const uint32_t base = (pair / D) * 2 * D, a = base + pair % D;
+      uint32_t* x = lds + a * 16;
+      uint32_t* y = lds + (a + D) * 16;
+      const uint32_t lm = skew(base + D - 1);
+      if (lm != Ops::MOD) ops.muladd(x, y, u, lm);
+      ops.xorin(y, x, u);
+    }
+    __syncthreads();
+  }
+}
+
+// GF(2^16) encode: grid x = axis, y = 64-byte chunk, z = square. LDS: n * 64 B.
+__global__ __launch_bounds__(256) void k_rs_encode_gf16(RsGeom g, const uint16_t* __restrict__ gexp,
+                                                        const uint16_t* __restrict__ glog,
+                                                        const uint16_t* __restrict__ gskew) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const uint32_t n = g.n;
+  const uint32_t coff = blockIdx.y * 64u;
+  const uint8_t* src = g.in + (uint64_t)blockIdx.z * g.in_sq + (uint64_t)blockIdx.x * g.in_axis + coff;
+  uint8_t* dst = g.out + (uint64_t)blockIdx.z * g.out_sq + (uint64_t)blockIdx.x * g.out_axis + coff;
+  for (uint32_t it = threadIdx.x; it < n * 4; it += blockDim.x) {
+    const uint32_t i = it >> 2, q = it & 3;
+    const uint4 v = reinterpret_cast<const uint4*>(src + (uint64_t)i * g.in_shard)[q];
+    reinterpret_cast<uint4*>(lds)[it] = v;
+    if (g.dcopy)
+      reinterpret_cast<uint4*>(g.dcopy + (uint64_t)blockIdx.z * g.dc_sq + (uint64_t)blockIdx.x * g.dc_axis + coff +
+                               (uint64_t)i * g.dc_shard)[q] = v;
+  }
+  __syncthreads();
+  Gf16Ops ops{gexp, glog};
+  auto skew = [&](uint32_t i) { return (uint32_t)gskew[i]; };
+  lds_ifft(ops, lds, n, n, skew);
+  lds_fft(ops, lds, n, skew);
+  for (uint32_t it = threadIdx.x; it < n * 4; it += blockDim.x) {
+    const uint32_t i = it >> 2, q = it & 3;
+    reinterpret_cast<uint4*>(dst + (uint64_t)i * g.out_shard)[q] = reinterpret_cast<const uint4*>(lds)[it];
+  }
+}
+
+template <int LOGK>
+static void launch_gf8(const RsGeom& g, const DeviceTables& t, hipStream_t s) {
+  dim3 grid(g.axes, (g.len + 511) / 512, g.nsq);
+  hipLaunchKernelGGL(k_rs_encode_gf8<LOGK>, grid, dim3(128), 0, s, g, t.tw8);
+}
+
+hipError_t launch_rs_encode(const RsGeom& g, const DeviceTables& t, hipStream_t s) {
+  if (g.axes == 0 || g.nsq == 0) return hipSuccess;
+  if (2 * g.n <= 256) {
+    switch (g.n) {
+      case 1: launch_gf8<0>(g, t, s); break;
+      case 2: launch_gf8<1>(g, t, s); break;
+      case 4: launch_gf8<2>(g, t, s); break;
+      case 8: launch_gf8<3>(g, t, s); break;
+      case 16: launch_gf8<4>(g, t, s); break;
+      case 32: launch_gf8<5>(g, t, s); break;
+      case 64: launch_gf8<6>(g, t, s); break;
+      case 128: launch_gf8<7>(g, t, s); break;
+      default: return hipErrorInvalidValue;
+    }
+  } else {
+    if (g.n > kMaxGf16Width) return hipErrorInvalidValue;
+    dim3 grid(g.axes, g.len / 64, g.nsq);
+    const size_t lds = (size_t)g.n * 64;
+    if (lds > 64 * 1024)
+      (void)hipFuncSetAttribute((const void*)k_rs_encode_gf16, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_rs_encode_gf16, grid, dim3(256), lds, s, g, t.exp16, t.log16, t.skew16);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_extend(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t nsq, const DeviceTables& t,
+                         hipStream_t s) {
+  const uint64_t row = (uint64_t)2 * k * kShare;  // bytes per EDS row
+  const uint64_t sq_eds = (uint64_t)4 * k * k * kShare;
+  const uint64_t sq_ods = (uint64_t)k * k * kShare;
+  hipError_t e;
+  // Q0 rows -> Q1 (reading the ODS and writing Q0 into the EDS on the way when ods != nullptr)
+  RsGeom rows{};
+  if (ods) {
+    rows.in = ods;
+    rows.in_sq = sq_ods;
+    rows.in_axis = (uint64_t)k * kShare;
+    rows.dcopy = eds;
+    rows.dc_sq = sq_eds;
+    rows.dc_axis = row;
+    rows.dc_shard = kShare;
+  } else {
+    rows.in = eds;
+    rows.in_sq = sq_eds;
+    rows.in_axis = row;
+  }
+  rows.in_shard = kShare;
+  rows.out = eds + (uint64_t)k * kShare;
+  rows.out_sq = sq_eds;
+  rows.out_axis = row;
+  rows.out_shard = kShare;
+  rows.n = k;
+  rows.len = kShare;
+  rows.axes = k;
+  rows.nsq = nsq;
+  if ((e = launch_rs_encode(rows, t, s)) != hipSuccess) return e;
+  // columns of [Q0|Q1] -> [Q2|Q3]
+  RsGeom cols{};
+  cols.in = eds;
+  cols.in_sq = sq_eds;
+  cols.in_axis = kShare;
+  cols.in_shard = row;
+  cols.out = eds + (uint64_t)k * row;
+  cols.out_sq = sq_eds;
+  cols.out_axis = kShare;
+  cols.out_shard = row;
+  cols.n = k;
+  cols.len = kShare;
+  cols.axes = 2 * k;
+  cols.nsq = nsq;
+  return launch_rs_encode(cols, t, s);
+}
+
+// ------------------------------------------------------------------ decode
+//
+// Leopard's error-locator erasure decoder (catid/leopard ReedSolomonDecode as used
+// by klauspost Reconstruct), over the n = 2m point domain with the recovery
+// (parity) shards at positions [0, m) and the original (data) shards at [m, 2m):
+//   err[i]   = sum_{e erased} log0[i ^ e]   (mod field modulus; log0 = log with log0[0] = 0)
+//              = log prod_{e erased, e != i} (w_i + w_e)
+//   work[i]  = present ? shard_i * exp(err[i]) : 0
+//   IFFT over all n points (offset 0), formal derivative, FFT over all n points
+//   erased i: shard_i = work[i] * exp(-err[i])
+// Erased parity shards are revealed by the same formula (the codeword is unique).
+
+template <class Ops, class SkewFn>
+__device__ void decode_chunk(const Ops& ops, uint32_t* lds, uint32_t* err, const uint8_t* pres, uint32_t m,
+                             SkewFn skew) {
+  const uint32_t n = 2 * m;
+  // work <- present * exp(err)
+  for (uint32_t it = threadIdx.x; it < n * Ops::UNITS; it += blockDim.x) {
+    const uint32_t i = it / Ops::UNITS, u = it % Ops::UNITS;
+    if (pres[i]) ops.scale(lds + i * 16, u, err[i]);
+  }
+  __syncthreads();
+  lds_ifft(ops, lds, n, 0, skew);
+  // formal derivative: new[x] = old[x] ^ xor_{t: bit t of x clear, x + 2^t < n} old[x + 2^t].
+  // Sources are never modified before being read in the sequential reference loop,
+  // so processing x in descending order of blocks is unnecessary: read old values
+  // for all targets first (per lane, a unit at a time), then write.
+  for (uint32_t base = 0; base < n * Ops::UNITS; base += blockDim.x) {
+    const uint32_t it = base + threadIdx.x;
+    uint32_t acc[2] = {0, 0};
+    const bool active = it < n * Ops::UNITS;
+    uint32_t x = 0, u = 0;
+    if (active) {
+      x = it / Ops::UNITS;
+      u = it % Ops::UNITS;
+      for (uint32_t t = 1; t < n; t <<= 1) {
+        if ((x & t) == 0 && x + t < n) {
+          acc[0] ^= lds[(x + t) * 16 + u];
+          if (Ops::UNITS == 8) acc[1] ^= lds[(x + t) * 16 + u + 8];
+        }
+      }
+    }
+    __syncthreads();
+    if (active) {
+      lds[x * 16 + u] ^= acc[0];
+      if (Ops::UNITS == 8) lds[x * 16 + u + 8] ^= acc[1];
+    }
+    __syncthreads();
+  }
+  lds_fft(ops, lds, n, skew);
+  for (uint32_t it = threadIdx.x; it < n * Ops::UNITS; it += blockDim.x) {
+    const uint32_t i = it / Ops::UNITS, u = it % Ops::UNITS;
+    if (!pres[i]) ops.scale(lds + i * 16, u, (Ops::MOD - err[i]) % Ops::MOD);
+  }
+  __syncthreads();
+}
+
+// grid: x = axis, y = 64-byte chunk. shards: [naxes][2m][len] in rsmt2d order
+// (data then parity); present: [naxes][2m].
+template <bool GF16>
+__global__ __launch_bounds__(256) void k_rs_decode(uint8_t* shards, const uint8_t* present, uint32_t m,
+                                                   uint32_t len, const uint16_t* __restrict__ gexp,
+                                                   const uint16_t* __restrict__ glog,
+                                                   const uint16_t* __restrict__ gskew) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const uint32_t n = 2 * m;
+  uint32_t* err = lds + n * 16;
+  uint8_t* pres = reinterpret_cast<uint8_t*>(err + n);
+  __shared__ uint8_t s_exp[256], s_log[256];
+  uint8_t* axis = shards + (uint64_t)blockIdx.x * n * len;
+  const uint8_t* pa = present + (uint64_t)blockIdx.x * n;
+  // position p in Leopard order: p < m -> parity shard p (rsmt2d index m + p); else data p - m.
+  for (uint32_t p = threadIdx.x; p < n; p += blockDim.x) pres[p] = pa[p < m ? m + p : p - m] ? 1 : 0;
+  if (!GF16) {
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
+      s_exp[i] = c_gf8.exp[i];
+      s_log[i] = c_gf8.log[i];
+    }
+  }
+  __syncthreads();
+  const uint32_t MOD = GF16 ? 65535u : 255u;
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    uint32_t acc = 0;
+    for (uint32_t e = 0; e < n; e++) {
+      if (pres[e]) continue;
+      const uint32_t x = i ^ e;
+      const uint32_t l = x == 0 ? 0u : (GF16 ? (uint32_t)glog[x] : (uint32_t)s_log[x]);
+      acc += l;
+      if (acc >= MOD) acc -= MOD;
+    }
+    err[i] = acc;
+  }
+  const uint32_t coff = blockIdx.y * 64u;
+  for (uint32_t it = threadIdx.x; it < n * 4; it += blockDim.x) {
+    const uint32_t p = it >> 2, q = it & 3;
+    const uint32_t r = p < m ? m + p : p - m;
+    reinterpret_cast<uint4*>(lds)[it] = reinterpret_cast<const uint4*>(axis + (uint64_t)r * len + coff)[q];
+  }
+  __syncthreads();
+  if (GF16) {
+    Gf16Ops ops{gexp, glog};
+    decode_chunk(ops, lds, err, pres, m, [&](uint32_t i) { return (uint32_t)gskew[i]; });
+  } else {
+    Gf8Ops ops{s_exp, s_log};
+    decode_chunk(ops, lds, err, pres, m, [&](uint32_t i) { return (uint32_t)c_gf8.skew[i]; });
+  }
+  for (uint32_t it = threadIdx.x; it < n * 4; it += blockDim.x) {
+    const uint32_t p = it >> 2, q = it & 3;
+    if (pres[p]) continue;
+    const uint32_t r = p < m ? m + p : p - m;
+    reinterpret_cast<uint4*>(axis + (uint64_t)r * len + coff)[q] = reinterpret_cast<const uint4*>(lds)[it];
+  }
+}
+
+size_t decode_workspace_size(uint32_t, uint32_t) { return 0; }
+
+hipError_t launch_rs_decode(uint8_t* shards, const uint8_t* present, uint32_t naxes, uint32_t m, uint32_t len,
+                            const DeviceTables& t, void*, hipStream_t s) {
+  if (!naxes) return hipSuccess;
+  hipError_t e = ensure_gf8_const();
+  if (e != hipSuccess) return e;
+  const uint32_t n = 2 * m;
+  const size_t lds = (size_t)n * 64 + (size_t)n * 4 + n;
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  dim3 grid(naxes, len / 64);
+  if (lds > 64 * 1024) {
+    (void)hipFuncSetAttribute((const void*)k_rs_decode<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)k_rs_decode<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  }
+  if (2 * m <= 256)
+    hipLaunchKernelGGL(k_rs_decode<false>, grid, dim3(256), lds, s, shards, present, m, len, t.exp16, t.log16,
+                       t.skew16);
+  else
+    hipLaunchKernelGGL(k_rs_decode<true>, grid, dim3(256), lds, s, shards, present, m, len, t.exp16, t.log16,
+                       t.skew16);
+  return hipGetLastError();
+}
+
+}  // namespace cel

@@ -1,0 +1,147 @@
+/*
+ * celestia_eds.h — C ABI of the MI355X-native extended-data-square hot path.
+ *
+ * This library replaces, behind an unchanged Go surface, the hot path of
+ * celestia-app's pkg/da (reference /root/reference):
+ *
+ *   da.ExtendShares                 pkg/da/data_availability_header.go:65-75
+ *   da.NewDataAvailabilityHeader    pkg/da/data_availability_header.go:44-63
+ *   DataAvailabilityHeader.Hash     pkg/da/data_availability_header.go:92-108
+ *   rsmt2d.Codec (LeoRSCodec)       pkg/appconsts/global_consts.go:92 (DefaultCodec)
+ *   rsmt2d.Tree via wrapper         pkg/wrapper/nmt_wrapper.go:14-17,83,93-124
+ *   rsmt2d ExtendedDataSquare.Repair (rsmt2d v0.14.0 [dep]; used by celestia-node)
+ *
+ * Every entry point returns cel_status (0 = OK) and never aborts. Buffers are
+ * borrowed for the duration of the call only (cgo forbids retaining Go pointers);
+ * outputs go to caller-allocated memory. A cel_ctx binds one HIP device and one
+ * stream; calls on one ctx are serialised internally, so a ctx may be shared by
+ * goroutines; use one ctx per device for concurrency.
+ *
+ * Layouts (all row-major, share = 512 B = appconsts.ShareSize):
+ *   ODS   k*k shares                         (the [][]byte of da.ExtendShares, flattened)
+ *   EDS   2k*2k shares                       (rsmt2d flattened square: Q0 Q1 / Q2 Q3)
+ *   roots 2k entries of 90 B                 (minNs(29) || maxNs(29) || sha256(32))
+ *   dah   32 B                               (RFC-6962 root of rowRoots || colRoots)
+ */
+#ifndef CELESTIA_EDS_H
+#define CELESTIA_EDS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int32_t cel_status;
+
+/* Status codes; each maps 1:1 onto a Go error of the reference surface. */
+#define CEL_OK 0
+#define CEL_EINVAL 1         /* bad argument (nil pointer, zero size)                          */
+#define CEL_ENOTPOW2 2       /* "number of shares is not a power of 2: got %d" (data_availability_header.go:68) */
+#define CEL_ECHUNK 3         /* chunk size not a positive multiple of 64 (rsmt2d ValidateChunkSize) */
+#define CEL_ETOOBIG 4        /* square wider than the device path supports                     */
+#define CEL_EORDER 5         /* nmt: leaves pushed out of namespace order (nmt_wrapper_test.go:106-111) */
+#define CEL_ETOOFEW 6        /* decode: fewer than k of 2k shards present                      */
+#define CEL_EBYZANTINE 7     /* rsmt2d ErrByzantineData: axis fails re-encoding or root check  */
+#define CEL_EUNREPAIRABLE 8  /* rsmt2d ErrUnrepairableDataSquare                               */
+#define CEL_EDEVICE 9        /* HIP runtime / kernel failure                                   */
+#define CEL_ENOMEM 10        /* device allocation failed                                       */
+#define CEL_ESHORT 11        /* "data is too short to contain namespace ID" (nmt_wrapper.go:98) */
+#define CEL_EPUSHPAST 12     /* "pushed past predetermined square size" (nmt_wrapper.go:95)     */
+
+/* Flags for the square entry points. */
+#define CEL_FLAG_ORDER_CHECK 0x1u   /* enforce the honest nmt push order (default in the Go path) */
+
+#define CEL_SHARE_SIZE 512u
+#define CEL_NAMESPACE_SIZE 29u
+#define CEL_NMT_NODE_SIZE 90u
+#define CEL_HASH_SIZE 32u
+
+typedef struct cel_ctx cel_ctx;
+
+/* ---------------------------------------------------------------- context */
+cel_status cel_ctx_create(int device, cel_ctx** out);
+void cel_ctx_destroy(cel_ctx* ctx);
+const char* cel_strerror(cel_status st);
+/* Go-style message of the last failing call on ctx (e.g. the exact
+ * "number of shares is not a power of 2: got 5" string). */
+const char* cel_last_error(const cel_ctx* ctx);
+/* Name of the device (for reports). */
+cel_status cel_device_name(cel_ctx* ctx, char* buf, size_t len);
+
+/* ------------------------------------------------------- square (host I/O) */
+/* da.ExtendShares + da.NewDataAvailabilityHeader in one device pass.
+ * shares: n_shares * share_size bytes (n_shares must be a power of two and a
+ * perfect square, i.e. k*k; replaces data_availability_header.go:65-75,44-63).
+ * eds_out may be NULL (PrepareProposal/ProcessProposal discard the EDS:
+ * app/prepare_proposal.go:81-83). row_roots/col_roots: 2k*90 B each; dah: 32 B. */
+cel_status cel_extend_shares(cel_ctx* ctx, const uint8_t* shares, uint32_t n_shares,
+                             uint32_t share_size, uint8_t* eds_out, uint8_t* row_roots,
+                             uint8_t* col_roots, uint8_t* dah, uint32_t flags);
+
+/* Batch replay: n independent k*k squares laid out back to back (config 4).
+ * eds_out (nullable): n * 4k^2 * share; roots: n * 2k * 90 each; dah: n * 32.
+ * status_out (nullable): per-square status (CEL_EORDER for a bad square). */
+cel_status cel_extend_batch(cel_ctx* ctx, const uint8_t* ods, uint32_t n, uint32_t k,
+                            uint32_t share_size, uint8_t* eds_out, uint8_t* row_roots,
+                            uint8_t* col_roots, uint8_t* dah, int32_t* status_out,
+                            uint32_t flags);
+
+/* -------------------------------------------------- square (device resident)
+ * Same as cel_extend_batch with every pointer in device memory of ctx's device.
+ * stream: a hipStream_t (NULL = ctx's own stream). Asynchronous: returns after
+ * enqueueing. d_status: n int32 (0 or CEL_EORDER). Required d_eds: n*4k^2*share
+ * (the EDS is always materialised on the device). d_work: scratch of
+ * cel_dev_workspace_size(k, n) bytes. */
+size_t cel_dev_workspace_size(uint32_t k, uint32_t n);
+cel_status cel_dev_extend_batch(cel_ctx* ctx, const void* d_ods, uint32_t n, uint32_t k,
+                                void* d_eds, void* d_row_roots, void* d_col_roots, void* d_dah,
+                                int32_t* d_status, void* d_work, void* stream, uint32_t flags);
+/* Phase entry points of the same pipeline (for profiling and the row-sharded
+ * multi-GPU mode): RS extension only, and NMT roots + DAH over a resident EDS. */
+cel_status cel_dev_extend_only(cel_ctx* ctx, const void* d_ods, uint32_t n, uint32_t k,
+                               void* d_eds, void* stream);
+cel_status cel_dev_commit_only(cel_ctx* ctx, const void* d_eds, uint32_t n, uint32_t k,
+                               void* d_row_roots, void* d_col_roots, void* d_dah,
+                               int32_t* d_status, void* d_work, void* stream, uint32_t flags);
+
+/* ------------------------------------------------------ rsmt2d.Codec surface
+ * Leopard RS (klauspost/reedsolomon v1.12.1 New(n, n, WithLeopardGF(true))):
+ * GF(2^8) when 2n <= 256, GF(2^16) otherwise. len must be a positive multiple
+ * of 64. data: n*len contiguous -> parity: n*len. */
+cel_status cel_codec_encode(cel_ctx* ctx, const uint8_t* data, uint32_t n, uint32_t len,
+                            uint8_t* parity);
+/* shards: 2n*len (n data then n parity), present: 2n flags (nil shard = 0).
+ * Fills every missing shard in place (rsmt2d Codec.Decode). */
+cel_status cel_codec_decode(cel_ctx* ctx, uint8_t* shards, const uint8_t* present, uint32_t n,
+                            uint32_t len);
+uint64_t cel_codec_max_chunks(void);             /* 32768 * 32768 */
+const char* cel_codec_name(void);                /* "Leopard" */
+cel_status cel_codec_validate_chunk_size(uint32_t len);
+
+/* ---------------------------------------------------- rsmt2d.Tree surface
+ * Root of one erasured NMT axis: the 2k cells of row/column `axis_index` of a
+ * square of original width k (wrapper.Push x 2k then Root,
+ * pkg/wrapper/nmt_wrapper.go:93-124). cells: 2k*share contiguous. */
+cel_status cel_axis_root(cel_ctx* ctx, const uint8_t* cells, uint32_t k, uint32_t axis_index,
+                         uint32_t share_size, uint8_t* root_out, uint32_t flags);
+/* Plain NMT root over n namespaced leaves of leaf_len bytes (ns = first 29 B). */
+cel_status cel_nmt_root(cel_ctx* ctx, const uint8_t* leaves, uint32_t n, uint32_t leaf_len,
+                        uint8_t* root_out, uint32_t flags);
+/* DataAvailabilityHeader.Hash: RFC-6962 root over rowRoots || colRoots (w each). */
+cel_status cel_dah_hash(cel_ctx* ctx, const uint8_t* row_roots, const uint8_t* col_roots,
+                        uint32_t w, uint8_t* out);
+
+/* ------------------------------------------------------------------ repair
+ * rsmt2d ExtendedDataSquare.Repair(rowRoots, colRoots): eds is 2k*2k*share with
+ * present[2k*2k] marking known cells. On CEL_OK every cell is filled. On
+ * CEL_EBYZANTINE, *bad_axis (0 = row, 1 = col) and *bad_index are set. */
+cel_status cel_repair(cel_ctx* ctx, uint8_t* eds, uint8_t* present, uint32_t k,
+                      uint32_t share_size, const uint8_t* row_roots, const uint8_t* col_roots,
+                      int32_t* bad_axis, int32_t* bad_index);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CELESTIA_EDS_H */

@@ -1,0 +1,53 @@
+"""GPU parity of the rsmt2d.Codec surface (Leopard encode/decode) against the oracle."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from eds_inputs import model_shards
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("k", [1, 2, 32, 128, 256, 512])
+def test_model_digest(ctx, golden, k):
+    from celestia_eds.rsmt2d import LeoRSCodec
+    codec = LeoRSCodec(ctx)
+    data = model_shards(k)
+    par = codec.Encode([d.tobytes() for d in data])
+    got = b"".join(par)
+    if str(k) in golden["leopard_model"]:
+        assert hashlib.sha256(got).hexdigest() == golden["leopard_model"][str(k)]["parity_sha256"]
+
+
+@pytest.mark.parametrize("n,ln", [(1, 64), (4, 64), (8, 192), (64, 512), (128, 512), (256, 128), (1024, 64)])
+def test_encode_matches_oracle(ctx, oracle, n, ln):
+    from celestia_eds.rsmt2d import LeoRSCodec
+    rng = np.random.default_rng(n * 7 + ln)
+    data = rng.integers(0, 256, (n, ln), dtype=np.uint8)
+    par = LeoRSCodec(ctx).Encode([d.tobytes() for d in data])
+    assert np.array_equal(np.frombuffer(b"".join(par), np.uint8).reshape(n, ln), oracle.rs_encode(data))
+
+
+@pytest.mark.parametrize("n", [1, 2, 8, 64, 128, 256, 512])
+def test_decode_random_erasures(ctx, oracle, n):
+    from celestia_eds.rsmt2d import LeoRSCodec
+    codec = LeoRSCodec(ctx)
+    rng = np.random.default_rng(n)
+    ln = 512 if n <= 128 else 64
+    data = rng.integers(0, 256, (n, ln), dtype=np.uint8)
+    cw = np.concatenate([data, oracle.rs_encode(data)])
+    for trial in range(3):
+        lost = set(rng.choice(2 * n, n, replace=False).tolist()) if trial else set(range(n))
+        shards = [None if i in lost else cw[i].tobytes() for i in range(2 * n)]
+        out = codec.Decode(shards)
+        assert np.array_equal(np.frombuffer(b"".join(out), np.uint8).reshape(2 * n, ln), cw)
+
+
+def test_decode_too_few(ctx):
+    from celestia_eds import CelError, _lib
+    from celestia_eds.rsmt2d import LeoRSCodec
+    shards = [bytes(64)] * 3 + [None] * 5
+    with pytest.raises(CelError) as ei:
+        LeoRSCodec(ctx).Decode(shards)
+    assert ei.value.status == _lib.ETOOFEW

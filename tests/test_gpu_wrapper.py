@@ -1,0 +1,74 @@
+"""GPU: pkg/wrapper behaviour (nmt_wrapper_test.go:19-128) through the device roots."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from eds_inputs import random_ods
+
+pytestmark = pytest.mark.gpu
+
+
+def erasured(oracle, k, seed):
+    data = random_ods(k, seed).reshape(-1, 512)[:k]  # k sorted namespaced shares
+    par = oracle.rs_encode(np.ascontiguousarray(data))
+    return [d.tobytes() for d in data] + [p.tobytes() for p in par]
+
+
+@pytest.mark.parametrize("k", [8, 128])
+def test_push_and_root_matches_oracle(ctx, oracle, k):
+    from celestia_eds.wrapper import NewErasuredNamespacedMerkleTree
+    cells = erasured(oracle, k, k)
+    tree = NewErasuredNamespacedMerkleTree(k, 0)
+    for c in cells:
+        tree.Push(c)
+    rc, exp = oracle.axis_root(np.frombuffer(b"".join(cells), np.uint8).reshape(2 * k, 512), k, 0)
+    assert rc == 0 and tree.Root() == exp
+
+
+def test_root_differs_from_plain_nmt(ctx, oracle):
+    from celestia_eds.wrapper import NewErasuredNamespacedMerkleTree
+    k = 8
+    data = [d.tobytes() for d in random_ods(4, 3).reshape(-1, 512)[:8]]
+    t = NewErasuredNamespacedMerkleTree(k, 0)
+    for d in data:
+        t.Push(d)
+    rc, plain = oracle.nmt_root([d[:29] + d for d in data])
+    assert rc == 0 and t.Root() != plain
+
+
+def test_empty_root_independent_of_params(ctx):
+    from celestia_eds.wrapper import NewErasuredNamespacedMerkleTree
+    r1 = NewErasuredNamespacedMerkleTree(1, 0).Root()
+    r2 = NewErasuredNamespacedMerkleTree(2, 1).Root()
+    assert r1 == r2 == bytes(58) + hashlib.sha256(b"").digest()
+
+
+def test_push_errors(ctx, oracle):
+    from celestia_eds import CelError
+    from celestia_eds.wrapper import NewErasuredNamespacedMerkleTree
+    k = 16
+    over = erasured(oracle, k + 1, 1)
+    t = NewErasuredNamespacedMerkleTree(k, 0)
+    with pytest.raises(CelError, match="pushed past predetermined square size"):
+        for d in over:
+            t.Push(d)
+    rev = sorted(erasured(oracle, k, 2), reverse=True)
+    t = NewErasuredNamespacedMerkleTree(k, 0)
+    with pytest.raises(CelError):
+        for d in rev:
+            t.Push(d)
+    t = NewErasuredNamespacedMerkleTree(k, 0)
+    with pytest.raises(CelError, match="data is too short to contain namespace ID"):
+        t.Push(b"\x01")
+
+
+def test_partial_tree_root(ctx, oracle):
+    """Root over fewer than 2k pushes goes through the generic device NMT."""
+    from celestia_eds.wrapper import NewErasuredNamespacedMerkleTree
+    data = [d.tobytes() for d in random_ods(4, 9).reshape(-1, 512)[:5]]
+    t = NewErasuredNamespacedMerkleTree(8, 0)
+    for d in data:
+        t.Push(d)
+    rc, exp = oracle.nmt_root([d[:29] + d for d in data])
+    assert rc == 0 and t.Root() == exp

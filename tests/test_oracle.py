@@ -1,0 +1,155 @@
+"""CPU: pin the oracle against the reference's own known answers before trusting it.
+
+- DAH known answers: pkg/da/data_availability_header_test.go:15-68
+- mainnet block 408 data root: x/blob/test/testdata/block_response.json (GF(2^8) pin)
+- Leopard table debug values and model digests: SURVEY.md Appendix A.2, A.3, A.5
+- scalar vs SIMD oracle paths, decode round trips, repair semantics
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from eds_inputs import constant_ods, model_shards, random_ods, tail_padding_share
+
+
+def test_gf8_debug_values(oracle):
+    l = oracle.lib()
+    assert [l.orc_gf_exp(8, i) for i in range(8)] == [1, 104, 92, 100, 114, 240, 86, 18]
+    assert [l.orc_gf_log(8, i) for i in range(8)] == [255, 0, 85, 170, 17, 68, 34, 136]
+    assert [l.orc_gf_skew(8, i) for i in range(16)] == [255, 255, 85, 255, 17, 85, 34, 255, 153, 17, 102, 85,
+                                                        51, 34, 187, 255]
+    assert [l.orc_gf_skew(8, i) for i in range(127, 135)] == [255, 160, 241, 29, 196, 167, 254, 144]
+    assert l.orc_gf_mul(8, 2, 3) == 1 and l.orc_gf_mul(8, 0x53, 0xCA) == 2
+
+
+def test_gf16_debug_values(oracle):
+    l = oracle.lib()
+    assert [l.orc_gf_exp(16, i) for i in range(8)] == [1, 18064, 26072, 25296, 22324, 17904, 21432, 7736]
+    assert [l.orc_gf_log(16, i) for i in range(8)] == [65535, 0, 21845, 43690, 17476, 4369, 34952, 8738]
+    assert [l.orc_gf_skew(16, i) for i in range(8)] == [65535, 65535, 21845, 65535, 17476, 21845, 34952, 65535]
+
+
+@pytest.mark.parametrize("k", [2, 32, 128, 256, 512])
+def test_leopard_model_digest(oracle, golden, k):
+    exp = golden["leopard_model"][str(k)]
+    for simd in (False, True):
+        oracle.set_simd(simd)
+        p = oracle.rs_encode(model_shards(k))
+        assert hashlib.sha256(p.tobytes()).hexdigest() == exp["parity_sha256"]
+        assert p[0, :8].tobytes().hex() == exp["parity0_head"]
+    oracle.set_simd(True)
+
+
+def test_sha256_paths(oracle):
+    rng = np.random.default_rng(0)
+    for n in [0, 1, 55, 56, 63, 64, 65, 181, 542, 1000]:
+        m = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        for simd in (False, True):
+            oracle.set_simd(simd)
+            assert oracle.sha256(m) == hashlib.sha256(m).digest()
+    oracle.set_simd(True)
+
+
+def test_dah_empty(oracle, golden):
+    z = np.zeros((0, 90), np.uint8)
+    assert oracle.dah_hash(z, z).hex() == golden["dah_known_answers"]["empty"]
+
+
+def test_dah_min(oracle, golden):
+    ods = np.frombuffer(tail_padding_share(), np.uint8).reshape(1, 1, 512)
+    assert oracle.extend_and_commit(ods)[3].hex() == golden["dah_known_answers"]["min"]
+
+
+@pytest.mark.parametrize("k,key", [(2, "typical_k2"), (128, "max_k128")])
+def test_dah_typical_and_max(oracle, golden, k, key):
+    _, _, _, dah = oracle.extend_and_commit(constant_ods(k), want_eds=False)
+    assert dah.hex() == golden["dah_known_answers"][key]
+
+
+def test_block408_data_root(oracle, golden, block408_ods):
+    g = golden["block408"]
+    assert hashlib.sha256(block408_ods.tobytes()).hexdigest() == g["ods_sha256"]
+    eds, rr, cr, dah = oracle.extend_and_commit(block408_ods)
+    assert dah.hex() == g["data_hash"]
+    assert hashlib.sha256(eds.tobytes()).hexdigest() == g["eds_sha256"]
+    assert rr[0].tobytes().hex() == g["row_root_0"] and cr[0].tobytes().hex() == g["col_root_0"]
+    assert rr[-1].tobytes().hex() == g["row_root_last"] and cr[-1].tobytes().hex() == g["col_root_last"]
+
+
+def test_q3_both_ways(oracle):
+    """specs/src/specs/data_structures.md:305: Q3 is the same extended from Q1 or Q2."""
+    k = 8
+    eds = oracle.extend(random_ods(k, 3))
+    q3_cols = np.stack([oracle.rs_encode(np.ascontiguousarray(eds[:k, k + c])) for c in range(k)], axis=1)
+    assert np.array_equal(q3_cols, eds[k:, k:])
+
+
+@pytest.mark.parametrize("n", [1, 2, 4, 16, 64, 128, 256])
+def test_decode_round_trip(oracle, n):
+    rng = np.random.default_rng(n)
+    ln = 64 if n >= 128 else 128
+    data = rng.integers(0, 256, (n, ln), dtype=np.uint8)
+    cw = np.concatenate([data, oracle.rs_encode(data)])
+    for trial in range(3):
+        present = np.ones(2 * n, np.uint8)
+        lost = rng.choice(2 * n, n, replace=False) if trial else np.arange(n)
+        present[lost] = 0
+        sh = cw.copy()
+        sh[present == 0] = 0
+        assert np.array_equal(oracle.rs_decode(sh, present), cw)
+
+
+def test_decode_too_few(oracle):
+    n = 4
+    sh = np.zeros((2 * n, 64), np.uint8)
+    present = np.zeros(2 * n, np.uint8)
+    present[: n - 1] = 1
+    with pytest.raises(ValueError):
+        oracle.rs_decode(sh, present)
+
+
+def test_repair_semantics(oracle):
+    k = 4
+    eds, rr, cr, _ = oracle.extend_and_commit(random_ods(k, 11))
+    w = 2 * k
+    # Q0 only (exactly 25%): always repairable
+    present = np.zeros((w, w), np.uint8)
+    present[:k, :k] = 1
+    damaged = eds.copy()
+    damaged[present == 0] = 0
+    rc, fixed, _, _ = oracle.repair(damaged, present, rr, cr)
+    assert rc == oracle.OK and np.array_equal(fixed, eds)
+    # too few cells: unrepairable
+    present = np.zeros((w, w), np.uint8)
+    present[0, :k - 1] = 1
+    rc, _, _, _ = oracle.repair(damaged, present, rr, cr)
+    assert rc == oracle.EUNREPAIRABLE
+    # one corrupted cell: byzantine
+    present = np.ones((w, w), np.uint8)
+    present[1, 1] = 0
+    bad = eds.copy()
+    bad[0, 0, 100] ^= 1
+    rc, _, _, (ba, bi) = oracle.repair(bad, present, rr, cr)
+    assert rc == oracle.EBYZANTINE and ba in (0, 1) and bi >= 0
+
+
+def test_nmt_empty_root(oracle):
+    rc, r = oracle.nmt_root([])
+    assert rc == 0 and r == bytes(58) + hashlib.sha256(b"").digest()
+
+
+def test_nmt_order_check(oracle):
+    a = b"\x00" * 28 + b"\x02" + b"x" * 10
+    b_ = b"\x00" * 28 + b"\x01" + b"y" * 10
+    assert oracle.nmt_root([a, b_])[0] == oracle.EORDER
+    assert oracle.nmt_root([b_, a])[0] == 0
+
+
+def test_roots_order_violation(oracle):
+    k = 4
+    ods = random_ods(k, 5)
+    ods[0, 0], ods[0, 1] = ods[0, 1].copy(), ods[0, 0].copy()
+    eds = oracle.extend(ods)
+    rc, _, _ = oracle.roots(eds, check_order=True)
+    assert rc == oracle.EORDER
