@@ -94,7 +94,7 @@ def main():
     assert (status == 0).all(), f"device reported status {status}"
 
     # ---- phase timing with HIP events on the launch stream (rank-local)
-    stream = torch.cuda.current_stream(dev)
+    stream = sb.hip_stream  # the stream every launch of `sb` goes to
 
     def timed(fn, reps):
         e0 = torch.cuda.Event(enable_timing=True)
@@ -171,6 +171,8 @@ def main():
             cores = len(os.sched_getaffinity(0))
         except AttributeError:
             pass
+        # the GPU box grants a CPU share (OMP_NUM_THREADS) far below the visible core count
+        cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
         oracle.set_threads(cores)
         n_done, t_cpu = 0, 0.0
         dah_dev = sb.dah.cpu().numpy()

@@ -32,9 +32,12 @@ class SquareBatch:
         self.status = torch.empty((n,), dtype=torch.int32, device=self.dev)
         ws = self.ctx.lib.cel_dev_workspace_size(k, n)
         self.work = torch.empty((ws,), dtype=torch.uint8, device=self.dev)
+        # A dedicated (non-null) stream: every launch of this batch goes there, and
+        # callers time it with events recorded on self.hip_stream.
+        self.hip_stream = torch.cuda.Stream(device=self.dev)
 
     def stream(self):
-        return ctypes.c_void_p(self.torch.cuda.current_stream(self.dev).cuda_stream)
+        return ctypes.c_void_p(self.hip_stream.cuda_stream)
 
     def extend_and_commit(self, order_check=True):
         c = self.ctx

@@ -10,9 +10,13 @@ pytestmark = pytest.mark.gpu
 
 
 def erasured(oracle, k, seed):
-    data = random_ods(k, seed).reshape(-1, 512)[:k]  # k sorted namespaced shares
+    """generateErasuredData (nmt_wrapper_test.go:143-151): k sorted namespaced shares
+    and their Leopard parity (k rounded up to a power of two for the codec)."""
+    kk = 1 << (k - 1).bit_length()
+    data = random_ods(kk, seed).reshape(-1, 512)[:kk]
     par = oracle.rs_encode(np.ascontiguousarray(data))
-    return [d.tobytes() for d in data] + [p.tobytes() for p in par]
+    return ([d.tobytes() for d in data] + [p.tobytes() for p in par])[: 2 * k] if kk == k else \
+        [d.tobytes() for d in data] + [p.tobytes() for p in par]
 
 
 @pytest.mark.parametrize("k", [8, 128])
@@ -29,11 +33,13 @@ def test_push_and_root_matches_oracle(ctx, oracle, k):
 def test_root_differs_from_plain_nmt(ctx, oracle):
     from celestia_eds.wrapper import NewErasuredNamespacedMerkleTree
     k = 8
-    data = [d.tobytes() for d in random_ods(4, 3).reshape(-1, 512)[:8]]
+    data = [d.tobytes() for d in random_ods(4, 3).reshape(-1, 512)[:8]]  # 8 of the 16 sorted shares
     t = NewErasuredNamespacedMerkleTree(k, 0)
     for d in data:
         t.Push(d)
-    rc, plain = oracle.nmt_root([d[:29] + d for d in data])
+    # nmt.New(...).Push(d) hashes d itself (its first 29 bytes are the namespace);
+    # the wrapper prefixes the namespace again (nmt_wrapper_test.go:49-73)
+    rc, plain = oracle.nmt_root(data)
     assert rc == 0 and t.Root() != plain
 
 
