@@ -91,6 +91,11 @@ cel_status cel_ctx_create(int device, cel_ctx** out) {
   ctx->device = device;
   DeviceGuard g(device);
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  for (int i = 0; i < cel_ctx::kPipe && e == hipSuccess; i++) {
+    e = hipStreamCreateWithFlags(&ctx->sub[i], hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_done[i], hipEventDisableTiming);
+  }
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_start, hipEventDisableTiming);
   if (e == hipSuccess) e = upload_tables(&ctx->tables);
   if (e != hipSuccess) {
     cel_ctx_destroy(ctx);
@@ -108,6 +113,11 @@ void cel_ctx_destroy(cel_ctx* ctx) {
     for (int i = 0; i < 6; i++)
       if (ctx->scratch[i]) (void)hipFree(ctx->scratch[i]);
     free_tables(&ctx->tables);
+    for (int i = 0; i < cel_ctx::kPipe; i++) {
+      if (ctx->sub[i]) (void)hipStreamDestroy(ctx->sub[i]);
+      if (ctx->ev_done[i]) (void)hipEventDestroy(ctx->ev_done[i]);
+    }
+    if (ctx->ev_start) (void)hipEventDestroy(ctx->ev_start);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   }
   delete ctx;
@@ -144,7 +154,21 @@ cel_status cel_device_name(cel_ctx* ctx, char* buf, size_t len) {
 
 // ------------------------------------------------------------------ squares
 
-size_t cel_dev_workspace_size(uint32_t k, uint32_t n) { return nmt_workspace_size(k, n); }
+// Chunking of a batch over the internal streams: chunk c runs RS extension then
+// NMT + DAH on stream sub[c], so chunk c+1's extension overlaps chunk c's hashing.
+static void pipe_plan(uint32_t n, uint32_t* chunk, uint32_t* nchunks) {
+  uint32_t nc = n < (uint32_t)cel_ctx::kPipe ? n : (uint32_t)cel_ctx::kPipe;
+  if (nc == 0) nc = 1;
+  *chunk = (n + nc - 1) / nc;
+  *nchunks = (n + *chunk - 1) / *chunk;
+}
+
+size_t cel_dev_workspace_size(uint32_t k, uint32_t n) {
+  uint32_t chunk, nchunks;
+  pipe_plan(n, &chunk, &nchunks);
+  const size_t a = nmt_workspace_size(k, n), b = (size_t)nchunks * nmt_workspace_size(k, chunk);
+  return a > b ? a : b;
+}
 
 static cel_status validate_square(cel_ctx* ctx, uint32_t k, uint32_t share_size) {
   if (share_size != kShare)
@@ -180,9 +204,32 @@ cel_status cel_dev_commit_only(cel_ctx* ctx, const void* d_eds, uint32_t n, uint
 cel_status cel_dev_extend_batch(cel_ctx* ctx, const void* d_ods, uint32_t n, uint32_t k, void* d_eds,
                                 void* d_row_roots, void* d_col_roots, void* d_dah, int32_t* d_status, void* d_work,
                                 void* stream, uint32_t flags) {
-  cel_status st = cel_dev_extend_only(ctx, d_ods, n, k, d_eds, stream);
+  if (!ctx || !d_eds || !n || !d_row_roots || !d_col_roots || !d_dah || !d_work) return CEL_EINVAL;
+  cel_status st = validate_square(ctx, k, kShare);
   if (st) return st;
-  return cel_dev_commit_only(ctx, d_eds, n, k, d_row_roots, d_col_roots, d_dah, d_status, d_work, stream, flags);
+  DeviceGuard g(ctx->device);
+  uint32_t chunk, nchunks;
+  pipe_plan(n, &chunk, &nchunks);
+  const size_t ws = nmt_workspace_size(k, chunk);
+  const uint64_t ods_sq = (uint64_t)k * k * kShare, eds_sq = 4 * ods_sq, roots_sq = (uint64_t)2 * k * kNode;
+  hipStream_t us = pick_stream(ctx, stream);
+  hipError_t e = hipEventRecord(ctx->ev_start, us);
+  for (uint32_t c = 0; c < nchunks && e == hipSuccess; c++) {
+    const uint32_t first = c * chunk, cnt = (first + chunk <= n) ? chunk : n - first;
+    hipStream_t s = ctx->sub[c];
+    if ((e = hipStreamWaitEvent(s, ctx->ev_start, 0)) != hipSuccess) break;
+    const uint8_t* ods = d_ods ? static_cast<const uint8_t*>(d_ods) + first * ods_sq : nullptr;
+    uint8_t* eds = static_cast<uint8_t*>(d_eds) + first * eds_sq;
+    if ((e = launch_extend(ods, eds, k, cnt, ctx->tables, s)) != hipSuccess) break;
+    e = launch_commit(eds, k, cnt, static_cast<uint8_t*>(d_row_roots) + first * roots_sq,
+                      static_cast<uint8_t*>(d_col_roots) + first * roots_sq, static_cast<uint8_t*>(d_dah) + first * 32,
+                      d_status ? d_status + first : nullptr, static_cast<uint8_t*>(d_work) + c * ws,
+                      (flags & CEL_FLAG_ORDER_CHECK) != 0, s);
+    if (e != hipSuccess) break;
+    if ((e = hipEventRecord(ctx->ev_done[c], s)) != hipSuccess) break;
+    e = hipStreamWaitEvent(us, ctx->ev_done[c], 0);
+  }
+  return e == hipSuccess ? CEL_OK : hip_fail(ctx, e, "extend batch");
 }
 
 cel_status cel_extend_batch(cel_ctx* ctx, const uint8_t* ods, uint32_t n, uint32_t k, uint32_t share_size,
@@ -201,7 +248,7 @@ cel_status cel_extend_batch(cel_ctx* ctx, const uint8_t* ods, uint32_t n, uint32
   if (!d_ods) return fail(ctx, CEL_ENOMEM, "device allocation failed");
   uint8_t* d_eds = static_cast<uint8_t*>(scratch(ctx, S_EDS, eds_b, &e));
   if (!d_eds) return fail(ctx, CEL_ENOMEM, "device allocation failed");
-  void* d_work = scratch(ctx, S_WORK, nmt_workspace_size(k, n), &e);
+  void* d_work = scratch(ctx, S_WORK, cel_dev_workspace_size(k, n), &e);
   if (!d_work) return fail(ctx, CEL_ENOMEM, "device allocation failed");
   uint8_t* d_out = static_cast<uint8_t*>(scratch(ctx, S_ROOTS, 2 * roots_b + (size_t)n * 32 + (size_t)n * 4, &e));
   if (!d_out) return fail(ctx, CEL_ENOMEM, "device allocation failed");
@@ -211,10 +258,8 @@ cel_status cel_extend_batch(cel_ctx* ctx, const uint8_t* ods, uint32_t n, uint32
   int32_t* d_st = reinterpret_cast<int32_t*>(d_out + 2 * roots_b + (size_t)n * 32);
   hipStream_t s = ctx->stream;
   if ((e = hipMemcpyAsync(d_ods, ods, ods_b, hipMemcpyHostToDevice, s)) != hipSuccess) return hip_fail(ctx, e, "H2D");
-  if ((e = launch_extend(d_ods, d_eds, k, n, ctx->tables, s)) != hipSuccess) return hip_fail(ctx, e, "extend");
-  if ((e = launch_commit(d_eds, k, n, d_rr, d_cr, d_dah, d_st, d_work, (flags & CEL_FLAG_ORDER_CHECK) != 0, s)) !=
-      hipSuccess)
-    return hip_fail(ctx, e, "commit");
+  st = cel_dev_extend_batch(ctx, d_ods, n, k, d_eds, d_rr, d_cr, d_dah, d_st, d_work, s, flags);
+  if (st) return st;
   if (eds_out && (e = hipMemcpyAsync(eds_out, d_eds, eds_b, hipMemcpyDeviceToHost, s)) != hipSuccess)
     return hip_fail(ctx, e, "D2H");
   std::vector<int32_t> stv(n);

@@ -93,8 +93,12 @@ size_t decode_workspace_size(uint32_t naxes, uint32_t n);
 
 // The opaque context of the C ABI.
 struct cel_ctx {
+  static constexpr int kPipe = 4;  // internal streams of the chunked batch pipeline
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t sub[kPipe] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev_start = nullptr;
+  hipEvent_t ev_done[kPipe] = {nullptr, nullptr, nullptr, nullptr};
   std::mutex mu;
   cel::DeviceTables tables;
   std::string last_error;

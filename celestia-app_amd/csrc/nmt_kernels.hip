@@ -13,7 +13,6 @@
 //              leaf is hashed once: 4k^2 x 9 compressions instead of the reference's
 //              8k^2 x 9. Also checks the honest push order on Q0.
 //   k_level  : one lane per inner node of one tree level, all 4k trees at once.
-//   k_top    : one wave per tree for the last <= 64 nodes (LDS, no launch per level).
 //   k_dah    : one workgroup per square, RFC-6962 over the 4k roots.
 // Nodes live on the device as 96-byte records (90 B node + 6 zero bytes) = 24 dwords.
 #include <hip/hip_runtime.h>
@@ -22,6 +21,24 @@
 
 #include "cel_internal.hpp"
 #include "sha256_device.hpp"
+
+// Minimum waves per SIMD requested from the register allocator (0 = compiler default).
+#ifndef CEL_LEAF_WAVES
+#define CEL_LEAF_WAVES 0
+#endif
+#ifndef CEL_LEVEL_WAVES
+#define CEL_LEVEL_WAVES 0
+#endif
+#if CEL_LEAF_WAVES > 0
+#define CEL_LEAF_BOUNDS __launch_bounds__(256, CEL_LEAF_WAVES)
+#else
+#define CEL_LEAF_BOUNDS __launch_bounds__(256)
+#endif
+#if CEL_LEVEL_WAVES > 0
+#define CEL_LEVEL_BOUNDS __launch_bounds__(256, CEL_LEVEL_WAVES)
+#else
+#define CEL_LEVEL_BOUNDS __launch_bounds__(256)
+#endif
 
 namespace cel {
 
@@ -60,46 +77,62 @@ __device__ __forceinline__ void put_digest(uint32_t (&nd)[kNodeWords], const uin
 // --------------------------------------------------------------------- leaves
 
 // Leaf message: 0x00 || ns(29) || share(512) = 542 B -> 9 blocks.
-// s = the share's little-endian dwords; ns = share[0:29] for Q0 cells, 0xFF*29 else.
-template <int B>
-__device__ __forceinline__ void leaf_block(uint32_t (&st)[8], const uint32_t* __restrict__ sh, bool q0) {
-  constexpr int BASE = (B == 0) ? 0 : 16 * B - 8;
-  constexpr int NW = (B == 8) ? 8 : 20;
-  uint32_t s[20];
-  const uint4* p4 = reinterpret_cast<const uint4*>(sh + BASE);
-#pragma unroll
-  for (int i = 0; i < NW / 4; i++) {
-    const uint4 v = p4[i];
-    s[4 * i] = v.x; s[4 * i + 1] = v.y; s[4 * i + 2] = v.z; s[4 * i + 3] = v.w;
-  }
+// sh = the share's little-endian dwords; ns = share[0:29] for Q0 cells, 0xFF*29 else.
+// Message word at byte p >= 32 is share bytes q..q+3 with q = p - 30 (q = 2 mod 4):
+// bytes 2,3 of dword (q-2)/4 and bytes 0,1 of the next -> one v_perm_b32 (and the
+// byte swap to big-endian comes for free in the same select).
+__device__ __forceinline__ void leaf_hash(uint32_t (&st)[8], const uint32_t* __restrict__ sh, bool q0) {
+  sha256_init(st);
   uint32_t w[16];
+  {  // block 0: 0x00 || ns || share[0:34]
+    uint32_t s[9];
+    const uint4* p4 = reinterpret_cast<const uint4*>(sh);
+    const uint4 v0 = p4[0], v1 = p4[1];
+    s[0] = v0.x; s[1] = v0.y; s[2] = v0.z; s[3] = v0.w; s[4] = v1.x; s[5] = v1.y; s[6] = v1.z; s[7] = v1.w;
+    s[8] = sh[8];
+    if (q0) {
+      w[0] = perm(0u, s[0], 0x0C000102u);
 #pragma unroll
-  for (int wi = 0; wi < 16; wi++) {
-    const int p = 64 * B + 4 * wi;
-    uint32_t x;
-    if (B == 0 && wi < 8) {
-      if (q0) {
-        if (wi == 0) x = perm(0u, s[0], 0x0C000102u);
-        else if (wi < 7) x = perm(s[wi - 1], s[wi], 0x07000102u);
-        else x = perm(s[6], s[7], 0x07000C0Cu) | perm(0u, s[0], 0x0C0C0001u);
-      } else {
-        if (wi == 0) x = 0x00FFFFFFu;
-        else if (wi < 7) x = 0xFFFFFFFFu;
-        else x = 0xFFFF0000u | perm(0u, s[0], 0x0C0C0001u);
-      }
-    } else if (p <= 536) {
-      const int a = (p - 32) / 4 - BASE;  // share dword holding bytes q, q+1 (q = p - 30)
-      x = perm(s[a], s[a + 1], 0x06070001u);
-    } else if (p == 540) {
-      x = perm(s[7], 0x80u, 0x0607000Cu);
-    } else if (p == 572) {
-      x = 542u * 8u;
+      for (int i = 1; i < 7; i++) w[i] = perm(s[i - 1], s[i], 0x07000102u);
+      w[7] = perm(s[6], s[7], 0x07000C0Cu) | perm(0u, s[0], 0x0C0C0001u);
     } else {
-      x = 0u;
+      w[0] = 0x00FFFFFFu;
+#pragma unroll
+      for (int i = 1; i < 7; i++) w[i] = 0xFFFFFFFFu;
+      w[7] = 0xFFFF0000u | perm(0u, s[0], 0x0C0C0001u);
     }
-    w[wi] = x;
+#pragma unroll
+    for (int i = 8; i < 16; i++) w[i] = perm(s[i - 8], s[i - 7], 0x06070001u);
+    sha256_compress(st, w);
   }
-  sha256_compress(st, w);
+#pragma unroll 1
+  for (int b = 1; b < 8; b++) {  // blocks 1..7: share bytes [64b-30, 64b+34)
+    const uint32_t* base = sh + 16 * b - 8;
+    const uint4* p4 = reinterpret_cast<const uint4*>(base);
+    uint32_t s[17];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const uint4 v = p4[i];
+      s[4 * i] = v.x; s[4 * i + 1] = v.y; s[4 * i + 2] = v.z; s[4 * i + 3] = v.w;
+    }
+    s[16] = base[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) w[i] = perm(s[i], s[i + 1], 0x06070001u);
+    sha256_compress(st, w);
+  }
+  {  // block 8: share[482:512] || 0x80 || 0... || len
+    const uint4* p4 = reinterpret_cast<const uint4*>(sh + 120);
+    uint32_t s[8];
+    const uint4 v0 = p4[0], v1 = p4[1];
+    s[0] = v0.x; s[1] = v0.y; s[2] = v0.z; s[3] = v0.w; s[4] = v1.x; s[5] = v1.y; s[6] = v1.z; s[7] = v1.w;
+#pragma unroll
+    for (int i = 0; i < 7; i++) w[i] = perm(s[i], s[i + 1], 0x06070001u);
+    w[7] = perm(s[7], 0x80u, 0x0607000Cu);
+#pragma unroll
+    for (int i = 8; i < 15; i++) w[i] = 0u;
+    w[15] = 542u * 8u;
+    sha256_compress(st, w);
+  }
 }
 
 // Namespace order: is ns(a) < ns(b)? (29-byte lexicographic compare of share prefixes)
@@ -125,7 +158,7 @@ __device__ __forceinline__ bool ns_less(const uint32_t* __restrict__ a, const ui
 
 // grid: x = cell block (256 cells), y = square. Writes leaf nodes [sq][W*W][24].
 template <bool ORDER>
-__global__ __launch_bounds__(256) void k_leaf(const uint8_t* __restrict__ eds, uint32_t k, uint32_t* __restrict__ leaves,
+__global__ CEL_LEAF_BOUNDS void k_leaf(const uint8_t* __restrict__ eds, uint32_t k, uint32_t* __restrict__ leaves,
                                               int32_t* __restrict__ bad_axis) {
   const uint32_t W = 2 * k;
   const uint32_t cell = blockIdx.x * 256u + threadIdx.x;
@@ -139,16 +172,7 @@ __global__ __launch_bounds__(256) void k_leaf(const uint8_t* __restrict__ eds, u
     if (r > 0 && ns_less(sh, sh - (uint64_t)W * kShare / 4)) atomicMin(bad_axis + blockIdx.y, (int32_t)(W + c));
   }
   uint32_t st[8];
-  sha256_init(st);
-  leaf_block<0>(st, sh, q0);
-  leaf_block<1>(st, sh, q0);
-  leaf_block<2>(st, sh, q0);
-  leaf_block<3>(st, sh, q0);
-  leaf_block<4>(st, sh, q0);
-  leaf_block<5>(st, sh, q0);
-  leaf_block<6>(st, sh, q0);
-  leaf_block<7>(st, sh, q0);
-  leaf_block<8>(st, sh, q0);
+  leaf_hash(st, sh, q0);
   uint32_t nd[kNodeWords];
   if (q0) {
     const uint4* p4 = reinterpret_cast<const uint4*>(sh);
@@ -215,7 +239,7 @@ __device__ __forceinline__ void hash_node(const uint32_t (&L)[kNodeWords], const
 //                tree t >= W is column t-W (children (2j, c), (2j+1, c)).
 //   otherwise  : in[sq][t][2j], in[sq][t][2j+1] with `nin` nodes per tree.
 template <bool FROM_LEAVES>
-__global__ __launch_bounds__(256) void k_level(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint32_t W,
+__global__ CEL_LEVEL_BOUNDS void k_level(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint32_t W,
                                                uint32_t nin, uint32_t trees) {
   const uint32_t nout = nin / 2;
   const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
@@ -236,51 +260,6 @@ __global__ __launch_bounds__(256) void k_level(const uint32_t* __restrict__ in, 
   load_node(in + ri * kNodeWords, R);
   hash_node(L, R, o);
   store_node(out + ((uint64_t)blockIdx.y * trees * nout + idx) * kNodeWords, o);
-}
-
-// Last <= 64 nodes of every tree: one 64-lane workgroup per tree (grid x = tree, y = square).
-// Odd counts carry the last node up unchanged (nmt / RFC-6962 split at the largest
-// power of two below n). Writes the root record to roots[sq][t].
-template <bool FROM_LEAVES>
-__global__ __launch_bounds__(64) void k_top(const uint32_t* __restrict__ in, uint32_t* __restrict__ roots, uint32_t W,
-                                            uint32_t nin, uint32_t trees) {
-  __shared__ __attribute__((aligned(16))) uint32_t s[64 * kNodeWords];
-  const uint32_t t = blockIdx.x, lane = threadIdx.x;
-  if (lane < nin) {
-    uint64_t li;
-    if (FROM_LEAVES) {
-      const uint64_t sq = (uint64_t)blockIdx.y * W * W;
-      li = (t < W) ? sq + (uint64_t)t * W + lane : sq + (uint64_t)lane * W + (t - W);
-    } else {
-      li = (uint64_t)blockIdx.y * trees * nin + (uint64_t)t * nin + lane;
-    }
-    const uint4* src = reinterpret_cast<const uint4*>(in + li * kNodeWords);
-    uint4* dst = reinterpret_cast<uint4*>(s + lane * kNodeWords);
-#pragma unroll
-    for (int i = 0; i < 6; i++) dst[i] = src[i];
-  }
-  __syncthreads();
-  uint32_t n = nin;
-  while (n > 1) {
-    const uint32_t half = n / 2;
-    uint32_t o[kNodeWords];
-    if (lane < half) {
-      uint32_t L[kNodeWords], R[kNodeWords];
-      load_node(s + (2 * lane) * kNodeWords, L);
-      load_node(s + (2 * lane + 1) * kNodeWords, R);
-      hash_node(L, R, o);
-    }
-    __syncthreads();
-    if (lane < half) store_node(s + lane * kNodeWords, o);
-    if ((n & 1) && lane == 0) {
-      uint4* dst = reinterpret_cast<uint4*>(s + half * kNodeWords);
-      const uint4* src = reinterpret_cast<const uint4*>(s + (n - 1) * kNodeWords);
-      for (int i = 0; i < 6; i++) dst[i] = src[i];
-    }
-    __syncthreads();
-    n = half + (n & 1);
-  }
-  if (lane < kNodeWords) roots[((uint64_t)blockIdx.y * trees + t) * kNodeWords + lane] = s[lane];
 }
 
 // ------------------------------------------------------------------ RFC-6962
@@ -433,25 +412,23 @@ hipError_t launch_commit(const uint8_t* eds, uint32_t k, uint32_t nsq, uint8_t* 
   if (order_check) hipLaunchKernelGGL(k_leaf<true>, gl, dim3(256), 0, s, eds, k, leaves, bad);
   else hipLaunchKernelGGL(k_leaf<false>, gl, dim3(256), 0, s, eds, k, leaves, bad);
 
+  // One launch per tree level, all 4k trees of all squares at once: every lane hashes
+  // one node, no idle lanes. The last level writes the root records.
   const uint32_t trees = 2 * W;
-  if (W <= 64) {
-    hipLaunchKernelGGL(k_top<true>, dim3(trees, nsq), dim3(64), 0, s, leaves, roots, W, W, trees);
-  } else {
-    uint32_t nin = W;
-    const uint32_t* src = leaves;
-    uint32_t* dst = ping;
-    bool first = true;
-    while (nin > 64) {
-      const uint32_t nout = nin / 2;
-      dim3 g((trees * nout + 255) / 256, nsq);
-      if (first) hipLaunchKernelGGL(k_level<true>, g, dim3(256), 0, s, src, dst, W, nin, trees);
-      else hipLaunchKernelGGL(k_level<false>, g, dim3(256), 0, s, src, dst, W, nin, trees);
-      first = false;
-      src = dst;
-      dst = (dst == ping) ? pong : ping;
-      nin = nout;
-    }
-    hipLaunchKernelGGL(k_top<false>, dim3(trees, nsq), dim3(64), 0, s, src, roots, W, nin, trees);
+  uint32_t nin = W;
+  const uint32_t* src = leaves;
+  uint32_t* dst = ping;
+  bool first = true;
+  while (nin > 1) {
+    const uint32_t nout = nin / 2;
+    uint32_t* out = (nout == 1) ? roots : dst;
+    dim3 g((trees * nout + 255) / 256, nsq);
+    if (first) hipLaunchKernelGGL(k_level<true>, g, dim3(256), 0, s, src, out, W, nin, trees);
+    else hipLaunchKernelGGL(k_level<false>, g, dim3(256), 0, s, src, out, W, nin, trees);
+    first = false;
+    src = out;
+    dst = (dst == ping) ? pong : ping;
+    nin = nout;
   }
   const size_t lds = (size_t)trees * 8 * 4;
   hipLaunchKernelGGL(k_merkle, dim3(nsq), dim3(256), lds, s, roots, trees, dah, row_roots, col_roots, bad, status);
@@ -514,16 +491,7 @@ __global__ __launch_bounds__(256) void k_axis_leaf(const uint8_t* __restrict__ c
   const uint32_t* sh = reinterpret_cast<const uint32_t*>(cells + (uint64_t)i * kShare);
   const bool q0 = (i < k) && (axis < k);
   uint32_t st[8];
-  sha256_init(st);
-  leaf_block<0>(st, sh, q0);
-  leaf_block<1>(st, sh, q0);
-  leaf_block<2>(st, sh, q0);
-  leaf_block<3>(st, sh, q0);
-  leaf_block<4>(st, sh, q0);
-  leaf_block<5>(st, sh, q0);
-  leaf_block<6>(st, sh, q0);
-  leaf_block<7>(st, sh, q0);
-  leaf_block<8>(st, sh, q0);
+  leaf_hash(st, sh, q0);
   uint32_t nd[kNodeWords];
   if (q0) {
     uint32_t s[8];
@@ -620,16 +588,7 @@ __global__ __launch_bounds__(256) void k_axes_leaf(const uint8_t* __restrict__ c
   const uint32_t* sh = reinterpret_cast<const uint32_t*>(cells + (uint64_t)g * kShare);
   const bool q0 = (i < k) && ((uint32_t)axis_idx[a] < k);
   uint32_t st[8];
-  sha256_init(st);
-  leaf_block<0>(st, sh, q0);
-  leaf_block<1>(st, sh, q0);
-  leaf_block<2>(st, sh, q0);
-  leaf_block<3>(st, sh, q0);
-  leaf_block<4>(st, sh, q0);
-  leaf_block<5>(st, sh, q0);
-  leaf_block<6>(st, sh, q0);
-  leaf_block<7>(st, sh, q0);
-  leaf_block<8>(st, sh, q0);
+  leaf_hash(st, sh, q0);
   uint32_t nd[kNodeWords];
   if (q0) {
     uint32_t s[8];
@@ -665,14 +624,14 @@ hipError_t launch_axes_roots(const uint8_t* cells, uint32_t k, const int32_t* ax
   uint32_t nin = W;
   const uint32_t* src = leaves;
   uint32_t* dst = ping;
-  while (nin > 64) {
+  while (nin > 1) {
     const uint32_t nout = nin / 2;
-    hipLaunchKernelGGL(k_level<false>, dim3((naxes * nout + 255) / 256, 1), dim3(256), 0, s, src, dst, W, nin, naxes);
-    src = dst;
+    uint32_t* out = (nout == 1) ? roots : dst;
+    hipLaunchKernelGGL(k_level<false>, dim3((naxes * nout + 255) / 256, 1), dim3(256), 0, s, src, out, W, nin, naxes);
+    src = out;
     dst = (dst == ping) ? pong : ping;
     nin = nout;
   }
-  hipLaunchKernelGGL(k_top<false>, dim3(naxes, 1), dim3(64), 0, s, src, roots, W, nin, naxes);
   return hipGetLastError();
 }
 

@@ -124,67 +124,127 @@ __device__ __forceinline__ uint32_t gf8_mul4(uint32_t y, const PermTab& t) {
   const uint32_t s0 = y & 0x07070707u;
   const uint32_t s1 = (y >> 3) & 0x07070707u;
   const uint32_t s2 = (y >> 6) & 0x03030303u;
-  return __builtin_amdgcn_perm(t.t0h, t.t0l, s0) ^ __builtin_amdgcn_perm(t.t1h, t.t1l, s1) ^
-         __builtin_amdgcn_perm(0u, t.t2, s2);
+  // v_bitop3 0x96 = three-input xor (gfx950)
+  return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_perm(t.t0h, t.t0l, s0), __builtin_amdgcn_perm(t.t1h, t.t1l, s1),
+                                     __builtin_amdgcn_perm(0u, t.t2, s2), 0x96);
 }
 
+// GF(2^8) encode, workgroup = G waves covering one 256-byte column slice of one
+// axis (lane = one dword column). K = 2^LOGK shards are split into G groups of
+// S = min(K, 32); wave g holds shards [S*g, S*g + S) in VGPRs ("arrangement A").
+//  - radix-2 layers with D < S are lane-local; their twiddle index depends on g
+//    only, so the product tables are scalar loads (wave-uniform);
+//  - for D >= S (only when G > 1) the group transposes through LDS so that every
+//    lane holds shards {l + S*h : h < G} for L = S/G values of l ("arrangement B");
+//    the twiddle index then depends on h only: uniform across the whole workgroup.
+// IFFT: A layers up, transpose, B layers up; FFT: B layers down, transpose back,
+// A layers down. LDS image [shard][lane] dwords: conflict-free (lane-contiguous).
 template <int LOGK>
-__device__ __forceinline__ void leo_encode_regs(uint32_t (&w)[1 << LOGK], const uint32_t* __restrict__ tw) {
-  constexpr int M = 1 << LOGK;
-  // IFFT over the data coset.
+__global__ __launch_bounds__(64 * ((LOGK > 5) ? (1 << (LOGK - 5)) : 1)) void k_rs_encode_gf8(
+    RsGeom g, const uint32_t* __restrict__ tw) {
+  constexpr int K = 1 << LOGK;
+  constexpr int LOGS = LOGK < 5 ? LOGK : 5;
+  constexpr int S = 1 << LOGS;
+  constexpr int G = K / S;
+  constexpr int L = S / G;
+  __shared__ uint32_t lds[G > 1 ? K * 64 : 1];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t col = blockIdx.y * 256u + (uint32_t)lane * 4u;
+  const bool active = col < g.len;
+  const uint8_t* src = g.in + (uint64_t)blockIdx.z * g.in_sq + (uint64_t)blockIdx.x * g.in_axis + col;
+  uint8_t* dst = g.out + (uint64_t)blockIdx.z * g.out_sq + (uint64_t)blockIdx.x * g.out_axis + col;
+  uint32_t w[S];
 #pragma unroll
-  for (int lg = 0; lg < LOGK; lg++) {
+  for (int i = 0; i < S; i++)
+    w[i] = active ? *reinterpret_cast<const uint32_t*>(src + (uint64_t)(wv * S + i) * g.in_shard) : 0u;
+  if (g.dcopy && active) {
+    uint8_t* dc = g.dcopy + (uint64_t)blockIdx.z * g.dc_sq + (uint64_t)blockIdx.x * g.dc_axis + col;
+#pragma unroll
+    for (int i = 0; i < S; i++) *reinterpret_cast<uint32_t*>(dc + (uint64_t)(wv * S + i) * g.dc_shard) = w[i];
+  }
+  // IFFT, arrangement A (D < S)
+#pragma unroll
+  for (int lg = 0; lg < LOGS; lg++) {
     const int D = 1 << lg;
 #pragma unroll
-    for (int base = 0; base < M; base += 2 * D) {
-      const PermTab t = load_tab(tw, M - 1 + base + D);
+    for (int base = 0; base < S; base += 2 * D) {
+      const PermTab t = load_tab(tw, K - 1 + wv * S + base + D);
 #pragma unroll
       for (int j = 0; j < D; j++) {
-        uint32_t& x = w[base + j];
-        uint32_t& y = w[base + j + D];
-        y ^= x;
-        x ^= gf8_mul4(y, t);
+        w[base + j + D] ^= w[base + j];
+        w[base + j] ^= gf8_mul4(w[base + j + D], t);
       }
     }
   }
-  // FFT over the parity coset.
+  if constexpr (G > 1) {
 #pragma unroll
-  for (int lg = LOGK - 1; lg >= 0; lg--) {
+    for (int i = 0; i < S; i++) lds[(wv * S + i) * 64 + lane] = w[i];
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < G; h++)
+#pragma unroll
+      for (int lo = 0; lo < L; lo++) w[h * L + lo] = lds[(wv * L + lo + S * h) * 64 + lane];
+    // IFFT, arrangement B (D = S << t): pairs (h, h + 2^t), twiddle from h only
+#pragma unroll
+    for (int t = 0; (1 << t) < G; t++) {
+      const int dh = 1 << t;
+#pragma unroll
+      for (int hb = 0; hb < G; hb += 2 * dh) {
+        const PermTab tb = load_tab(tw, K - 1 + S * hb + S * dh);
+#pragma unroll
+        for (int h = hb; h < hb + dh; h++)
+#pragma unroll
+          for (int lo = 0; lo < L; lo++) {
+            w[(h + dh) * L + lo] ^= w[h * L + lo];
+            w[h * L + lo] ^= gf8_mul4(w[(h + dh) * L + lo], tb);
+          }
+      }
+    }
+    // FFT, arrangement B
+#pragma unroll
+    for (int t = 0; (1 << t) < G; t++) {
+      const int dh = G >> (t + 1);
+#pragma unroll
+      for (int hb = 0; hb < G; hb += 2 * dh) {
+        const PermTab tb = load_tab(tw, S * hb + S * dh - 1);
+#pragma unroll
+        for (int h = hb; h < hb + dh; h++)
+#pragma unroll
+          for (int lo = 0; lo < L; lo++) {
+            w[h * L + lo] ^= gf8_mul4(w[(h + dh) * L + lo], tb);
+            w[(h + dh) * L + lo] ^= w[h * L + lo];
+          }
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < G; h++)
+#pragma unroll
+      for (int lo = 0; lo < L; lo++) lds[(wv * L + lo + S * h) * 64 + lane] = w[h * L + lo];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < S; i++) w[i] = lds[(wv * S + i) * 64 + lane];
+  } else {
+    // single group: the IFFT high layers are the remaining A layers (none when K == S)
+  }
+  // FFT, arrangement A (D < S)
+#pragma unroll
+  for (int lg = LOGS - 1; lg >= 0; lg--) {
     const int D = 1 << lg;
 #pragma unroll
-    for (int base = 0; base < M; base += 2 * D) {
-      const PermTab t = load_tab(tw, base + D - 1);
+    for (int base = 0; base < S; base += 2 * D) {
+      const PermTab t = load_tab(tw, wv * S + base + D - 1);
 #pragma unroll
       for (int j = 0; j < D; j++) {
-        uint32_t& x = w[base + j];
-        uint32_t& y = w[base + j + D];
-        x ^= gf8_mul4(y, t);
-        y ^= x;
+        w[base + j] ^= gf8_mul4(w[base + j + D], t);
+        w[base + j + D] ^= w[base + j];
       }
     }
   }
-}
-
-// grid: x = axis, y = 512-byte slice of the shard, z = square. block: 128 lanes,
-// lane t owns bytes [4t, 4t+4) of the slice in every shard of the axis.
-template <int LOGK>
-__global__ __launch_bounds__(128) void k_rs_encode_gf8(RsGeom g, const uint32_t* __restrict__ tw) {
-  constexpr int M = 1 << LOGK;
-  const uint32_t off = blockIdx.y * 512u + threadIdx.x * 4u;
-  if (off >= g.len) return;
-  const uint8_t* src = g.in + (uint64_t)blockIdx.z * g.in_sq + (uint64_t)blockIdx.x * g.in_axis + off;
-  uint8_t* dst = g.out + (uint64_t)blockIdx.z * g.out_sq + (uint64_t)blockIdx.x * g.out_axis + off;
-  uint32_t w[M];
+  if (active) {
 #pragma unroll
-  for (int i = 0; i < M; i++) w[i] = *reinterpret_cast<const uint32_t*>(src + (uint64_t)i * g.in_shard);
-  if (g.dcopy) {
-    uint8_t* dc = g.dcopy + (uint64_t)blockIdx.z * g.dc_sq + (uint64_t)blockIdx.x * g.dc_axis + off;
-#pragma unroll
-    for (int i = 0; i < M; i++) *reinterpret_cast<uint32_t*>(dc + (uint64_t)i * g.dc_shard) = w[i];
+    for (int i = 0; i < S; i++) *reinterpret_cast<uint32_t*>(dst + (uint64_t)(wv * S + i) * g.out_shard) = w[i];
   }
-  leo_encode_regs<LOGK>(w, tw);
-#pragma unroll
-  for (int i = 0; i < M; i++) *reinterpret_cast<uint32_t*>(dst + (uint64_t)i * g.out_shard) = w[i];
 }
 
 // ------------------------------------------------- LDS transform kernels
@@ -328,8 +388,9 @@ __global__ __launch_bounds__(256) void k_rs_encode_gf16(RsGeom g, const uint16_t
 
 template <int LOGK>
 static void launch_gf8(const RsGeom& g, const DeviceTables& t, hipStream_t s) {
-  dim3 grid(g.axes, (g.len + 511) / 512, g.nsq);
-  hipLaunchKernelGGL(k_rs_encode_gf8<LOGK>, grid, dim3(128), 0, s, g, t.tw8);
+  constexpr int threads = 64 * ((LOGK > 5) ? (1 << (LOGK - 5)) : 1);
+  dim3 grid(g.axes, (g.len + 255) / 256, g.nsq);
+  hipLaunchKernelGGL(k_rs_encode_gf8<LOGK>, grid, dim3(threads), 0, s, g, t.tw8);
 }
 
 hipError_t launch_rs_encode(const RsGeom& g, const DeviceTables& t, hipStream_t s) {
