@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <cstdlib>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -91,9 +92,10 @@ cel_status cel_ctx_create(int device, cel_ctx** out) {
   ctx->device = device;
   DeviceGuard g(device);
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
-  for (int i = 0; i < cel_ctx::kPipe && e == hipSuccess; i++) {
-    e = hipStreamCreateWithFlags(&ctx->sub[i], hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_done[i], hipEventDisableTiming);
+  for (int i = 0; i < cel_ctx::kPipe && e == hipSuccess; i++) e = hipStreamCreateWithFlags(&ctx->sub[i], hipStreamNonBlocking);
+  for (int i = 0; i < cel_ctx::kChunks && e == hipSuccess; i++) {
+    e = hipEventCreateWithFlags(&ctx->ev_done[i], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_rs[i], hipEventDisableTiming);
   }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_start, hipEventDisableTiming);
   if (e == hipSuccess) e = upload_tables(&ctx->tables);
@@ -113,9 +115,11 @@ void cel_ctx_destroy(cel_ctx* ctx) {
     for (int i = 0; i < 6; i++)
       if (ctx->scratch[i]) (void)hipFree(ctx->scratch[i]);
     free_tables(&ctx->tables);
-    for (int i = 0; i < cel_ctx::kPipe; i++) {
+    for (int i = 0; i < cel_ctx::kPipe; i++)
       if (ctx->sub[i]) (void)hipStreamDestroy(ctx->sub[i]);
+    for (int i = 0; i < cel_ctx::kChunks; i++) {
       if (ctx->ev_done[i]) (void)hipEventDestroy(ctx->ev_done[i]);
+      if (ctx->ev_rs[i]) (void)hipEventDestroy(ctx->ev_rs[i]);
     }
     if (ctx->ev_start) (void)hipEventDestroy(ctx->ev_start);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -154,10 +158,30 @@ cel_status cel_device_name(cel_ctx* ctx, char* buf, size_t len) {
 
 // ------------------------------------------------------------------ squares
 
-// Chunking of a batch over the internal streams: chunk c runs RS extension then
-// NMT + DAH on stream sub[c], so chunk c+1's extension overlaps chunk c's hashing.
+// Chunking of a batch over the internal streams: chunk c runs RS extension then NMT +
+// DAH on stream sub[c % kPipe]. Extensions are chained (chunk c+1's starts when chunk
+// c's ends) so each runs on the whole chip while earlier chunks hash: the VALU-bound
+// hashing of chunk c overlaps the extension of chunk c+1, and only the last chunk's
+// latency-bound tree top + DAH is exposed. CEL_PIPE_CHUNKS overrides the chunk count.
+static uint32_t pipe_chunks_default() {
+  static const uint32_t v = [] {
+    const char* e = getenv("CEL_PIPE_CHUNKS");
+    const int x = e ? atoi(e) : 2;
+    return (uint32_t)(x < 1 ? 1 : (x > cel_ctx::kChunks ? cel_ctx::kChunks : x));
+  }();
+  return v;
+}
+
+static bool pipe_stagger() {
+  static const bool v = [] {
+    const char* e = getenv("CEL_PIPE_STAGGER");
+    return e && atoi(e) != 0;
+  }();
+  return v;
+}
+
 static void pipe_plan(uint32_t n, uint32_t* chunk, uint32_t* nchunks) {
-  uint32_t nc = n < (uint32_t)cel_ctx::kPipe ? n : (uint32_t)cel_ctx::kPipe;
+  uint32_t nc = n < pipe_chunks_default() ? n : pipe_chunks_default();
   if (nc == 0) nc = 1;
   *chunk = (n + nc - 1) / nc;
   *nchunks = (n + *chunk - 1) / *chunk;
@@ -216,11 +240,13 @@ cel_status cel_dev_extend_batch(cel_ctx* ctx, const void* d_ods, uint32_t n, uin
   hipError_t e = hipEventRecord(ctx->ev_start, us);
   for (uint32_t c = 0; c < nchunks && e == hipSuccess; c++) {
     const uint32_t first = c * chunk, cnt = (first + chunk <= n) ? chunk : n - first;
-    hipStream_t s = ctx->sub[c];
+    hipStream_t s = ctx->sub[c % cel_ctx::kPipe];
     if ((e = hipStreamWaitEvent(s, ctx->ev_start, 0)) != hipSuccess) break;
+    if (c > 0 && pipe_stagger() && (e = hipStreamWaitEvent(s, ctx->ev_rs[c - 1], 0)) != hipSuccess) break;
     const uint8_t* ods = d_ods ? static_cast<const uint8_t*>(d_ods) + first * ods_sq : nullptr;
     uint8_t* eds = static_cast<uint8_t*>(d_eds) + first * eds_sq;
     if ((e = launch_extend(ods, eds, k, cnt, ctx->tables, s)) != hipSuccess) break;
+    if ((e = hipEventRecord(ctx->ev_rs[c], s)) != hipSuccess) break;
     e = launch_commit(eds, k, cnt, static_cast<uint8_t*>(d_row_roots) + first * roots_sq,
                       static_cast<uint8_t*>(d_col_roots) + first * roots_sq, static_cast<uint8_t*>(d_dah) + first * 32,
                       d_status ? d_status + first : nullptr, static_cast<uint8_t*>(d_work) + c * ws,

@@ -50,6 +50,7 @@ void free_tables(DeviceTables* t);
 
 // Kernel launchers (rs_kernels.hip / nmt_kernels.hip). All asynchronous on `s`.
 hipError_t launch_rs_encode(const RsGeom& g, const DeviceTables& t, hipStream_t s);
+hipError_t launch_rs_encode_bitslice(const RsGeom& g, hipStream_t s);  // GF(2^8), n <= 128
 // Full 2D extension of nsq squares: Q0 rows -> Q1, then all 2k columns -> Q2|Q3.
 // ods == nullptr means Q0 is already in place inside eds.
 hipError_t launch_extend(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t nsq,
@@ -93,12 +94,14 @@ size_t decode_workspace_size(uint32_t naxes, uint32_t n);
 
 // The opaque context of the C ABI.
 struct cel_ctx {
-  static constexpr int kPipe = 4;  // internal streams of the chunked batch pipeline
+  static constexpr int kPipe = 4;     // internal streams of the chunked batch pipeline
+  static constexpr int kChunks = 16;  // max chunks per batch call
   int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t sub[kPipe] = {nullptr, nullptr, nullptr, nullptr};
   hipEvent_t ev_start = nullptr;
-  hipEvent_t ev_done[kPipe] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev_done[kChunks] = {};
+  hipEvent_t ev_rs[kChunks] = {};
   std::mutex mu;
   cel::DeviceTables tables;
   std::string last_error;

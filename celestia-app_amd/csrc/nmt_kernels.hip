@@ -238,9 +238,14 @@ __device__ __forceinline__ void hash_node(const uint32_t (&L)[kNodeWords], const
 //   FROM_LEAVES: tree t < W is row t (children leaves (t, 2j), (t, 2j+1));
 //                tree t >= W is column t-W (children (2j, c), (2j+1, c)).
 //   otherwise  : in[sq][t][2j], in[sq][t][2j+1] with `nin` nodes per tree.
+__device__ __forceinline__ void rfc_leaf90(const uint32_t (&R)[kNodeWords], uint32_t (&st)[8]);
+
+// One tree level for all trees. With LEAFD != nullptr this is the root level: each lane
+// also hashes its root as an RFC-6962 leaf of the DAH tree (2 compressions) so the
+// per-square DAH kernel starts from leaf digests.
 template <bool FROM_LEAVES>
 __global__ CEL_LEVEL_BOUNDS void k_level(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint32_t W,
-                                               uint32_t nin, uint32_t trees) {
+                                               uint32_t nin, uint32_t trees, uint32_t* __restrict__ leafd) {
   const uint32_t nout = nin / 2;
   const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
   if (idx >= trees * nout) return;
@@ -259,7 +264,15 @@ __global__ CEL_LEVEL_BOUNDS void k_level(const uint32_t* __restrict__ in, uint32
   load_node(in + li * kNodeWords, L);
   load_node(in + ri * kNodeWords, R);
   hash_node(L, R, o);
-  store_node(out + ((uint64_t)blockIdx.y * trees * nout + idx) * kNodeWords, o);
+  const uint64_t oi = (uint64_t)blockIdx.y * trees * nout + idx;
+  store_node(out + oi * kNodeWords, o);
+  if (leafd) {
+    uint32_t st[8];
+    rfc_leaf90(o, st);
+    uint4* d = reinterpret_cast<uint4*>(leafd + oi * 8);
+    d[0] = make_uint4(st[0], st[1], st[2], st[3]);
+    d[1] = make_uint4(st[4], st[5], st[6], st[7]);
+  }
 }
 
 // ------------------------------------------------------------------ RFC-6962
@@ -316,18 +329,23 @@ __device__ __forceinline__ void sha_empty(uint32_t (&st)[8]) {
 
 // One workgroup per item list: items[g][n] 96-byte records -> 32-byte root (BE words in
 // out[g*8..]). Also packs the first n items into 90-byte outputs (row/col roots) if given.
-__global__ __launch_bounds__(256) void k_merkle(const uint32_t* __restrict__ items, uint32_t n, uint8_t* __restrict__ dah,
-                                                uint8_t* __restrict__ row_out, uint8_t* __restrict__ col_out,
-                                                const int32_t* __restrict__ bad_axis, int32_t* __restrict__ status) {
+__global__ __launch_bounds__(256) void k_merkle(const uint32_t* __restrict__ items, const uint32_t* __restrict__ leafd,
+                                                uint32_t n, uint8_t* __restrict__ dah, uint8_t* __restrict__ row_out,
+                                                uint8_t* __restrict__ col_out, const int32_t* __restrict__ bad_axis,
+                                                int32_t* __restrict__ status) {
   extern __shared__ __attribute__((aligned(16))) uint32_t hs[];  // n * 8 words
   const uint32_t g = blockIdx.x;
   const uint32_t* it = items + (uint64_t)g * n * kNodeWords;
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-    uint32_t R[kNodeWords], st[8];
-    load_node(it + (uint64_t)i * kNodeWords, R);
-    rfc_leaf90(R, st);
+  if (leafd) {
+    for (uint32_t i = threadIdx.x; i < n * 8; i += blockDim.x) hs[i] = leafd[(uint64_t)g * n * 8 + i];
+  } else {
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+      uint32_t R[kNodeWords], st[8];
+      load_node(it + (uint64_t)i * kNodeWords, R);
+      rfc_leaf90(R, st);
 #pragma unroll
-    for (int j = 0; j < 8; j++) hs[i * 8 + j] = st[j];
+      for (int j = 0; j < 8; j++) hs[i * 8 + j] = st[j];
+    }
   }
   // pack 90-byte roots (first half rows, second half columns)
   if (row_out) {
@@ -385,11 +403,12 @@ __global__ void k_fill_i32(int32_t* p, uint32_t n, int32_t v) {
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // Workspace: leaves [nsq][W*W] nodes | ping [nsq][2W][W/2] | pong [nsq][2W][W/4] |
-//            roots [nsq][2W] nodes | bad_axis [nsq] int32
+//            roots [nsq][2W] nodes | bad_axis [nsq] int32 | DAH leaf digests [nsq][2W][8]
 size_t nmt_workspace_size(uint32_t k, uint32_t nsq) {
   const size_t W = 2 * (size_t)k, nb = kNodeWords * 4;
   return align256(nsq * W * W * nb) + align256(nsq * 2 * W * (W / 2 + 1) * nb) +
-         align256(nsq * 2 * W * (W / 4 + 1) * nb) + align256(nsq * 2 * W * nb) + align256(nsq * 4 + 4);
+         align256(nsq * 2 * W * (W / 4 + 1) * nb) + align256(nsq * 2 * W * nb) + align256(nsq * 4 + 4) +
+         align256(nsq * 2 * W * 32);
 }
 
 hipError_t launch_commit(const uint8_t* eds, uint32_t k, uint32_t nsq, uint8_t* row_roots, uint8_t* col_roots,
@@ -406,6 +425,8 @@ hipError_t launch_commit(const uint8_t* eds, uint32_t k, uint32_t nsq, uint8_t* 
   uint32_t* roots = reinterpret_cast<uint32_t*>(base);
   base += align256((size_t)nsq * 2 * W * nb);
   int32_t* bad = reinterpret_cast<int32_t*>(base);
+  base += align256((size_t)nsq * 4 + 4);
+  uint32_t* leafd = reinterpret_cast<uint32_t*>(base);
 
   hipLaunchKernelGGL(k_fill_i32, dim3((nsq + 255) / 256), dim3(256), 0, s, bad, nsq, INT_MAX);
   dim3 gl((W * W + 255) / 256, nsq);
@@ -422,16 +443,17 @@ hipError_t launch_commit(const uint8_t* eds, uint32_t k, uint32_t nsq, uint8_t* 
   while (nin > 1) {
     const uint32_t nout = nin / 2;
     uint32_t* out = (nout == 1) ? roots : dst;
+    uint32_t* ld = (nout == 1) ? leafd : nullptr;
     dim3 g((trees * nout + 255) / 256, nsq);
-    if (first) hipLaunchKernelGGL(k_level<true>, g, dim3(256), 0, s, src, out, W, nin, trees);
-    else hipLaunchKernelGGL(k_level<false>, g, dim3(256), 0, s, src, out, W, nin, trees);
+    if (first) hipLaunchKernelGGL(k_level<true>, g, dim3(256), 0, s, src, out, W, nin, trees, ld);
+    else hipLaunchKernelGGL(k_level<false>, g, dim3(256), 0, s, src, out, W, nin, trees, ld);
     first = false;
     src = out;
     dst = (dst == ping) ? pong : ping;
     nin = nout;
   }
   const size_t lds = (size_t)trees * 8 * 4;
-  hipLaunchKernelGGL(k_merkle, dim3(nsq), dim3(256), lds, s, roots, trees, dah, row_roots, col_roots, bad, status);
+  hipLaunchKernelGGL(k_merkle, dim3(nsq), dim3(256), lds, s, roots, leafd, trees, dah, row_roots, col_roots, bad, status);
   return hipGetLastError();
 }
 
@@ -627,7 +649,8 @@ hipError_t launch_axes_roots(const uint8_t* cells, uint32_t k, const int32_t* ax
   while (nin > 1) {
     const uint32_t nout = nin / 2;
     uint32_t* out = (nout == 1) ? roots : dst;
-    hipLaunchKernelGGL(k_level<false>, dim3((naxes * nout + 255) / 256, 1), dim3(256), 0, s, src, out, W, nin, naxes);
+    hipLaunchKernelGGL(k_level<false>, dim3((naxes * nout + 255) / 256, 1), dim3(256), 0, s, src, out, W, nin, naxes,
+                       nullptr);
     src = out;
     dst = (dst == ping) ? pong : ping;
     nin = nout;
@@ -651,7 +674,7 @@ hipError_t launch_merkle_root(const uint8_t* items, uint32_t n, uint32_t item_le
   if (n) hipLaunchKernelGGL(k_pad_items, dim3((n + 255) / 256), dim3(256), 0, s, items, n, item_len, pad);
   const size_t lds = (size_t)(n ? n : 1) * 8 * 4;
   if (lds > 64 * 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_merkle, dim3(1), dim3(256), lds, s, pad, n, out, nullptr, nullptr, nullptr, nullptr);
+  hipLaunchKernelGGL(k_merkle, dim3(1), dim3(256), lds, s, pad, nullptr, n, out, nullptr, nullptr, nullptr, nullptr);
   return hipGetLastError();
 }
 

@@ -22,6 +22,8 @@
 // barrier per layer.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "cel_internal.hpp"
@@ -393,8 +395,30 @@ static void launch_gf8(const RsGeom& g, const DeviceTables& t, hipStream_t s) {
   hipLaunchKernelGGL(k_rs_encode_gf8<LOGK>, grid, dim3(threads), 0, s, g, t.tw8);
 }
 
+// GF(2^8) implementation. Bit-sliced for n <= 16 (one shard group per lane: 172 VGPRs,
+// no LDS exchange); v_perm tables for n >= 32, where the bit-sliced kernel needs the
+// whole 256 KiB granule set of a workgroup in registers (256 VGPRs, one workgroup per
+// CU) and its load/compute/store phases stop overlapping (profiles/r1_rs_impl_ab.txt).
+// CEL_RS_IMPL=perm|bitslice forces one implementation for every n.
+static int gf8_impl_override() {
+  static const int v = [] {
+    const char* e = getenv("CEL_RS_IMPL");
+    if (!e) return 0;
+    if (std::string(e) == "perm") return 1;
+    if (std::string(e) == "bitslice") return 2;
+    return 0;
+  }();
+  return v;
+}
+static bool use_perm_gf8(uint32_t n) {
+  const int o = gf8_impl_override();
+  if (o) return o == 1;
+  return n >= 32;
+}
+
 hipError_t launch_rs_encode(const RsGeom& g, const DeviceTables& t, hipStream_t s) {
   if (g.axes == 0 || g.nsq == 0) return hipSuccess;
+  if (2 * g.n <= 256 && !use_perm_gf8(g.n) && g.len % 32 == 0) return launch_rs_encode_bitslice(g, s);
   if (2 * g.n <= 256) {
     switch (g.n) {
       case 1: launch_gf8<0>(g, t, s); break;
