@@ -1,0 +1,180 @@
+// Package celestiaeds binds libcelestia_eds.so (MI355X / gfx950) behind the
+// reference's own Go surface. It is a sketch of the cgo stub a celestia-app
+// maintainer would add; this repository's build image has no Go toolchain, so it
+// is not compiled or tested here (parity is established through the C ABI tests).
+//
+// Replaces, without changing signatures:
+//   pkg/da/data_availability_header.go:65  da.ExtendShares
+//   pkg/da/data_availability_header.go:44  da.NewDataAvailabilityHeader (roots precomputed)
+//   pkg/appconsts/global_consts.go:92       appconsts.DefaultCodec (rsmt2d.Codec)
+package celestiaeds
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../../include
+#cgo LDFLAGS: -L${SRCDIR}/../../celestia-app_amd -lcelestia_eds -Wl,-rpath,${SRCDIR}/../../celestia-app_amd
+#include <stdlib.h>
+#include "celestia_eds.h"
+*/
+import "C"
+
+import (
+	"errors"
+	"fmt"
+	"sync"
+	"unsafe"
+)
+
+const (
+	ShareSize    = C.CEL_SHARE_SIZE
+	NmtNodeSize  = C.CEL_NMT_NODE_SIZE
+	flagOrder    = C.CEL_FLAG_ORDER_CHECK
+)
+
+// Status codes map 1:1 onto the reference's Go errors (include/celestia_eds.h).
+var (
+	ErrNotPow2       = errors.New("number of shares is not a power of 2")
+	ErrByzantineData = errors.New("byzantine data")
+	ErrUnrepairable  = errors.New("failed to solve data square")
+)
+
+type Context struct {
+	mu  sync.Mutex
+	ctx *C.cel_ctx
+}
+
+func NewContext(device int) (*Context, error) {
+	var c *C.cel_ctx
+	if st := C.cel_ctx_create(C.int(device), &c); st != C.CEL_OK {
+		return nil, fmt.Errorf("cel_ctx_create: %s", C.GoString(C.cel_strerror(st)))
+	}
+	return &Context{ctx: c}, nil
+}
+
+func (c *Context) Close() { C.cel_ctx_destroy(c.ctx) }
+
+func (c *Context) err(st C.cel_status) error {
+	if st == C.CEL_OK {
+		return nil
+	}
+	msg := C.GoString(C.cel_last_error(c.ctx))
+	switch st {
+	case C.CEL_ENOTPOW2:
+		return fmt.Errorf("%w: %s", ErrNotPow2, msg)
+	case C.CEL_EBYZANTINE:
+		return fmt.Errorf("%w: %s", ErrByzantineData, msg)
+	case C.CEL_EUNREPAIRABLE:
+		return ErrUnrepairable
+	}
+	return errors.New(msg)
+}
+
+// ExtendShares is the device pass behind da.ExtendShares: the [][]byte ODS is copied
+// into one contiguous buffer (cgo may not retain Go pointers), extended on the GPU, and
+// the flattened EDS plus all 4k roots and the DAH hash come back in one call.
+// The caller wraps the result with rsmt2d.ImportExtendedDataSquare(flat, codec,
+// RootTableConstructor(rowRoots, colRoots)) so NewDataAvailabilityHeader is unchanged.
+func (c *Context) ExtendShares(shares [][]byte) (flat []byte, rowRoots, colRoots [][]byte, dah []byte, err error) {
+	n := len(shares)
+	buf := C.malloc(C.size_t(n * ShareSize))
+	defer C.free(buf)
+	dst := unsafe.Slice((*byte)(buf), n*ShareSize)
+	for i, s := range shares {
+		copy(dst[i*ShareSize:], s)
+	}
+	k := 1
+	for k*k < n {
+		k <<= 1
+	}
+	w := 2 * k
+	flat = make([]byte, w*w*ShareSize)
+	rr := make([]byte, w*NmtNodeSize)
+	cr := make([]byte, w*NmtNodeSize)
+	dah = make([]byte, 32)
+	c.mu.Lock()
+	st := C.cel_extend_shares(c.ctx, (*C.uint8_t)(buf), C.uint32_t(n), ShareSize,
+		(*C.uint8_t)(unsafe.Pointer(&flat[0])), (*C.uint8_t)(unsafe.Pointer(&rr[0])),
+		(*C.uint8_t)(unsafe.Pointer(&cr[0])), (*C.uint8_t)(unsafe.Pointer(&dah[0])), flagOrder)
+	c.mu.Unlock()
+	if err = c.err(st); err != nil {
+		return nil, nil, nil, nil, err
+	}
+	for i := 0; i < w; i++ {
+		rowRoots = append(rowRoots, rr[i*NmtNodeSize:(i+1)*NmtNodeSize])
+		colRoots = append(colRoots, cr[i*NmtNodeSize:(i+1)*NmtNodeSize])
+	}
+	return flat, rowRoots, colRoots, dah, nil
+}
+
+// Codec implements rsmt2d.Codec (Encode/Decode/MaxChunks/Name/ValidateChunkSize) on
+// the device; rsmt2d's per-axis calls pay one launch each, so the square path above
+// is the fast path and this exists for API completeness (e.g. Repair from celestia-node).
+type Codec struct{ C *Context }
+
+func (cd Codec) Name() string    { return C.GoString(C.cel_codec_name()) }
+func (cd Codec) MaxChunks() int  { return int(C.cel_codec_max_chunks()) }
+func (cd Codec) ValidateChunkSize(n int) error {
+	if C.cel_codec_validate_chunk_size(C.uint32_t(n)) != C.CEL_OK {
+		return fmt.Errorf("chunkSize %d must be a multiple of 64 bytes", n)
+	}
+	return nil
+}
+
+func (cd Codec) Encode(data [][]byte) ([][]byte, error) {
+	n, l := len(data), len(data[0])
+	in := C.malloc(C.size_t(n * l))
+	out := C.malloc(C.size_t(n * l))
+	defer C.free(in)
+	defer C.free(out)
+	src := unsafe.Slice((*byte)(in), n*l)
+	for i, d := range data {
+		copy(src[i*l:], d)
+	}
+	cd.C.mu.Lock()
+	st := C.cel_codec_encode(cd.C.ctx, (*C.uint8_t)(in), C.uint32_t(n), C.uint32_t(l), (*C.uint8_t)(out))
+	cd.C.mu.Unlock()
+	if err := cd.C.err(st); err != nil {
+		return nil, err
+	}
+	par := unsafe.Slice((*byte)(out), n*l)
+	res := make([][]byte, n)
+	for i := range res {
+		res[i] = append([]byte(nil), par[i*l:(i+1)*l]...)
+	}
+	return res, nil
+}
+
+func (cd Codec) Decode(shards [][]byte) ([][]byte, error) {
+	n2 := len(shards)
+	l := 0
+	for _, s := range shards {
+		if s != nil {
+			l = len(s)
+			break
+		}
+	}
+	buf := C.malloc(C.size_t(n2 * l))
+	pres := C.malloc(C.size_t(n2))
+	defer C.free(buf)
+	defer C.free(pres)
+	b := unsafe.Slice((*byte)(buf), n2*l)
+	p := unsafe.Slice((*byte)(pres), n2)
+	for i, s := range shards {
+		if s != nil {
+			copy(b[i*l:], s)
+			p[i] = 1
+		} else {
+			p[i] = 0
+		}
+	}
+	cd.C.mu.Lock()
+	st := C.cel_codec_decode(cd.C.ctx, (*C.uint8_t)(buf), (*C.uint8_t)(pres), C.uint32_t(n2/2), C.uint32_t(l))
+	cd.C.mu.Unlock()
+	if err := cd.C.err(st); err != nil {
+		return nil, err
+	}
+	out := make([][]byte, n2)
+	for i := range out {
+		out[i] = append([]byte(nil), b[i*l:(i+1)*l]...)
+	}
+	return out, nil
+}
