@@ -37,8 +37,12 @@ struct RsGeom {
   uint32_t nsq;   // squares
 };
 
+constexpr uint32_t kTw16Words = 20;    // dwords of one GF(2^16) v_perm product table
+constexpr uint32_t kTw16Count = 4096;  // skew indices covered (2n - 1 < 4096 for n <= 2048)
+
 struct DeviceTables {
   uint32_t* tw8 = nullptr;     // [255][8] GF(2^8) twiddle product tables, indexed by skew index
+  uint32_t* tw16 = nullptr;    // [kTw16Count][kTw16Words] GF(2^16) product tables, by skew index
   uint16_t* exp16 = nullptr;   // [65536]
   uint16_t* log16 = nullptr;   // [65536]
   uint16_t* skew16 = nullptr;  // [65535]

@@ -48,10 +48,37 @@ static void perm_table8(const LeoField& f, uint32_t lm, uint32_t out[8]) {
   for (uint32_t n = 0; n < 4; n++) out[4] |= mul(n << 6) << (8 * n);
 }
 
+// GF(2^16) product tables for the v_perm multiply by c = exp(lm): the 16-bit input
+// symbol splits into six fields (lo byte bits 0-2, 3-5, 6-7; hi byte likewise);
+// for each field a table of the low and of the high product byte, as v_perm
+// operands (8 entries = 2 dwords, 4 entries = 1 dword). Layout (dwords):
+//   [0,1] lo0->L  [2,3] lo0->H  [4,5] lo3->L  [6,7] lo3->H  [8] lo6->L  [9] lo6->H
+//   [10..19] the same for the hi byte.  lm == 65535 (zero twiddle) gives zeros.
+static void perm_table16(const LeoField& f, uint32_t lm, uint32_t out[kTw16Words]) {
+  for (uint32_t i = 0; i < kTw16Words; i++) out[i] = 0;
+  if (lm == f.mod) return;
+  for (int half = 0; half < 2; half++) {
+    uint32_t* o = out + 10 * half;
+    for (uint32_t n = 0; n < 8; n++) {
+      const uint32_t p0 = f.mul_log(n << (8 * half), lm), p1 = f.mul_log(n << (8 * half + 3), lm);
+      o[0 + (n >> 2)] |= (p0 & 0xFF) << (8 * (n & 3));
+      o[2 + (n >> 2)] |= (p0 >> 8) << (8 * (n & 3));
+      o[4 + (n >> 2)] |= (p1 & 0xFF) << (8 * (n & 3));
+      o[6 + (n >> 2)] |= (p1 >> 8) << (8 * (n & 3));
+    }
+    for (uint32_t n = 0; n < 4; n++) {
+      const uint32_t p2 = f.mul_log(n << (8 * half + 6), lm);
+      o[8] |= (p2 & 0xFF) << (8 * n);
+      o[9] |= (p2 >> 8) << (8 * n);
+    }
+  }
+}
+
 hipError_t upload_tables(DeviceTables* t) {
   const LeoField& f8 = leo_gf8();
   const LeoField& f16 = leo_gf16();
-  std::vector<uint32_t> tw(255 * 8), mul8(256 * 8);
+  std::vector<uint32_t> tw(255 * 8), mul8(256 * 8), tw16((size_t)kTw16Count * kTw16Words);
+  for (uint32_t i = 0; i < kTw16Count; i++) perm_table16(f16, f16.skew[i], &tw16[(size_t)i * kTw16Words]);
   for (uint32_t i = 0; i < 255; i++) perm_table8(f8, f8.skew[i], &tw[i * 8]);
   for (uint32_t lm = 0; lm < 256; lm++) perm_table8(f8, lm == 255 ? 0 : lm, &mul8[lm * 8]);
   // mul8[255] is "multiply by exp(255) = 1" (a real log value, not the skew sentinel)
@@ -67,6 +94,8 @@ hipError_t upload_tables(DeviceTables* t) {
   }
   hipError_t e;
   if ((e = hipMalloc(&t->tw8, tw.size() * 4)) != hipSuccess) return e;
+  if ((e = hipMalloc(&t->tw16, tw16.size() * 4)) != hipSuccess) return e;
+  if ((e = hipMemcpy(t->tw16, tw16.data(), tw16.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return e;
   if ((e = hipMalloc(&t->mul8, mul8.size() * 4)) != hipSuccess) return e;
   if ((e = hipMalloc(&t->exp16, 65536 * 2)) != hipSuccess) return e;
   if ((e = hipMalloc(&t->log16, 65536 * 2)) != hipSuccess) return e;
@@ -80,6 +109,7 @@ hipError_t upload_tables(DeviceTables* t) {
 
 void free_tables(DeviceTables* t) {
   (void)hipFree(t->tw8);
+  (void)hipFree(t->tw16);
   (void)hipFree(t->mul8);
   (void)hipFree(t->exp16);
   (void)hipFree(t->log16);
@@ -247,6 +277,252 @@ __global__ __launch_bounds__(64 * ((LOGK > 5) ? (1 << (LOGK - 5)) : 1)) void k_r
 #pragma unroll
     for (int i = 0; i < S; i++) *reinterpret_cast<uint32_t*>(dst + (uint64_t)(wv * S + i) * g.out_shard) = w[i];
   }
+}
+
+
+// ------------------------------------------------ GF(2^16) register encode
+//
+// Same schedule as k_rs_encode_gf8 (wave g owns shards [32g, 32g+32) in VGPRs, layers
+// with D < 32 lane-local with wave-uniform twiddles, layers D >= 32 after an LDS
+// transpose with workgroup-uniform twiddles) but a lane holds 4 GF(2^16) symbols per
+// shard: the lo-byte dword and the matching hi-byte dword of Leopard's 64-byte
+// lo/hi block layout (sym[j] = b[j] | b[j+32] << 8). Lane l covers
+// block l/8, dword l%8, so one workgroup (K/32 waves) is exactly one 512-byte slice of
+// one axis. The multiply is twelve v_perm lookups (3+3+2-bit fields of both bytes,
+// low and high product byte) in SGPR-resident product tables.
+struct Perm16 {
+  uint32_t t[kTw16Words];
+};
+
+// One product table into VGPRs: five 16-byte vector loads from an address every lane
+// shares (an L1/L2 broadcast). Scalar loads would put 20 SGPRs per live table under
+// pressure, and gfx950 VOP3 reads at most one SGPR, so v_perm needs VGPR tables anyway.
+// `dep` is the last value the previous butterfly block wrote: a fake data dependency
+// that pins the load after that block (otherwise the DAG scheduler issues every table
+// load of a phase up front and spills them).
+__device__ __forceinline__ Perm16 load_tab16(const uint32_t* __restrict__ tw, int idx, uint32_t dep) {
+  uint32_t off = (uint32_t)idx * (kTw16Words * 4);
+  asm volatile("" : "+v"(off) : "v"(dep));
+  const uint4* p = reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(tw) + off);
+  Perm16 r;
+#pragma unroll
+  for (int i = 0; i < (int)kTw16Words / 4; i++) {
+    const uint4 v = p[i];
+    r.t[4 * i] = v.x;
+    r.t[4 * i + 1] = v.y;
+    r.t[4 * i + 2] = v.z;
+    r.t[4 * i + 3] = v.w;
+  }
+  return r;
+}
+
+// Materialise a value: stops the combiner from folding "(a ^ b) & mask" of the next
+// layer's field extraction into v_bitop3 of the un-xored inputs, which keeps both
+// inputs of every butterfly alive across layers and spills.
+// asm volatile statements keep their order, so pinning the inputs of every butterfly
+// (pin2) and its outputs (opaque) sequences the butterflies: the SelectionDAG
+// scheduler otherwise interleaves the field extraction of all butterflies of a layer.
+__device__ __forceinline__ void opaque(uint32_t& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void pin2(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d) {
+  asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+}
+
+// x ^= y * c for 4 symbols held as (lo dword, hi dword).
+__device__ __forceinline__ void gf16_muladd4(uint32_t& xl, uint32_t& xh, uint32_t yl, uint32_t yh, const Perm16& T) {
+  const uint32_t a0 = yl & 0x07070707u, a1 = (yl >> 3) & 0x07070707u, a2 = (yl >> 6) & 0x03030303u;
+  const uint32_t b0 = yh & 0x07070707u, b1 = (yh >> 3) & 0x07070707u, b2 = (yh >> 6) & 0x03030303u;
+  const uint32_t* t = T.t;
+  const uint32_t l0 = __builtin_amdgcn_perm(t[1], t[0], a0), l1 = __builtin_amdgcn_perm(t[5], t[4], a1);
+  const uint32_t l2 = __builtin_amdgcn_perm(0u, t[8], a2), l3 = __builtin_amdgcn_perm(t[11], t[10], b0);
+  const uint32_t l4 = __builtin_amdgcn_perm(t[15], t[14], b1), l5 = __builtin_amdgcn_perm(0u, t[18], b2);
+  const uint32_t h0 = __builtin_amdgcn_perm(t[3], t[2], a0), h1 = __builtin_amdgcn_perm(t[7], t[6], a1);
+  const uint32_t h2 = __builtin_amdgcn_perm(0u, t[9], a2), h3 = __builtin_amdgcn_perm(t[13], t[12], b0);
+  const uint32_t h4 = __builtin_amdgcn_perm(t[17], t[16], b1), h5 = __builtin_amdgcn_perm(0u, t[19], b2);
+  xl = __builtin_amdgcn_bitop3_b32(xl, __builtin_amdgcn_bitop3_b32(l0, l1, l2, 0x96),
+                                   __builtin_amdgcn_bitop3_b32(l3, l4, l5, 0x96), 0x96);
+  xh = __builtin_amdgcn_bitop3_b32(xh, __builtin_amdgcn_bitop3_b32(h0, h1, h2, 0x96),
+                                   __builtin_amdgcn_bitop3_b32(h3, h4, h5, 0x96), 0x96);
+}
+
+template <int LOGK>
+__global__ __launch_bounds__(64 * (1 << (LOGK - 5))) void k_rs_encode_gf16p(RsGeom g, const uint32_t* __restrict__ tw) {
+  constexpr int K = 1 << LOGK;
+  constexpr int S = 32;
+  constexpr int LOGS = 5;
+  constexpr int G = K / S;
+  constexpr int L = S / G;
+  extern __shared__ uint32_t lds[];  // [K][64] dwords: one half (lo or hi) of the image
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // every lane is active: the launcher requires len % 512 == 0
+  const uint32_t col = blockIdx.y * 512u + (uint32_t)(lane >> 3) * 64u + (uint32_t)(lane & 7) * 4u;
+  // buffer resources: scalar base per (square, axis), 32-bit lane offset, scalar shard offset
+  const __amdgpu_buffer_rsrc_t rin =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(g.in + (uint64_t)blockIdx.z * g.in_sq +
+                                                             (uint64_t)blockIdx.x * g.in_axis),
+                                        0, 0x7fffffff, 0x00020000);
+  const uint32_t in_shard = (uint32_t)g.in_shard, out_shard = (uint32_t)g.out_shard;
+  uint32_t wl[S], wh[S];
+#pragma unroll
+  for (int i = 0; i < S; i++) {
+    const uint32_t so = (uint32_t)(wv * S + i) * in_shard;
+    wl[i] = __builtin_amdgcn_raw_buffer_load_b32(rin, col, so, 0);
+    wh[i] = __builtin_amdgcn_raw_buffer_load_b32(rin, col + 32, so, 0);
+  }
+  if (g.dcopy) {
+    const __amdgpu_buffer_rsrc_t rdc = __builtin_amdgcn_make_buffer_rsrc(
+        g.dcopy + (uint64_t)blockIdx.z * g.dc_sq + (uint64_t)blockIdx.x * g.dc_axis, 0, 0x7fffffff, 0x00020000);
+    const uint32_t dc_shard = (uint32_t)g.dc_shard;
+#pragma unroll
+    for (int i = 0; i < S; i++) {
+      const uint32_t so = (uint32_t)(wv * S + i) * dc_shard;
+      __builtin_amdgcn_raw_buffer_store_b32(wl[i], rdc, col, so, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(wh[i], rdc, col + 32, so, 0);
+    }
+  }
+  uint32_t last = wh[S - 1];
+  // IFFT, arrangement A (D < S): twiddle from the wave's group only
+#pragma unroll
+  for (int lg = 0; lg < LOGS; lg++) {
+    const int D = 1 << lg;
+#pragma unroll
+    for (int base = 0; base < S; base += 2 * D) {
+      const Perm16 t = load_tab16(tw, K - 1 + wv * S + base + D, last);
+#pragma unroll
+      for (int j = 0; j < D; j++) {
+        pin2(wl[base + j], wh[base + j], wl[base + j + D], wh[base + j + D]);
+        wl[base + j + D] ^= wl[base + j];
+        wh[base + j + D] ^= wh[base + j];
+        gf16_muladd4(wl[base + j], wh[base + j], wl[base + j + D], wh[base + j + D], t);
+        opaque(wl[base + j]);
+        opaque(wh[base + j]);
+        last = wh[base + j];
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // A -> B: lane holds shards {lo_abs + S*h : h < G} for L values lo_abs = wv*L + lo
+  auto exchange = [&](bool to_b) {
+#pragma unroll
+    for (int half = 0; half < 2; half++) {
+      uint32_t* w = half ? wh : wl;
+#pragma unroll
+      for (int i = 0; i < S; i++) {
+        const int shard = to_b ? (wv * S + i) : (wv * L + (i % L) + S * (i / L));
+        lds[shard * 64 + lane] = w[i];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < S; i++) {
+        const int shard = to_b ? (wv * L + (i % L) + S * (i / L)) : (wv * S + i);
+        w[i] = lds[shard * 64 + lane];
+      }
+      __syncthreads();
+    }
+  };
+  exchange(true);
+  last = wh[S - 1];
+  // IFFT, arrangement B (D = S << t): pairs (h, h + 2^t), twiddle from h only
+#pragma unroll
+  for (int t = 0; (1 << t) < G; t++) {
+    const int dh = 1 << t;
+#pragma unroll
+    for (int hb = 0; hb < G; hb += 2 * dh) {
+      const Perm16 tb = load_tab16(tw, K - 1 + S * hb + S * dh, last);
+#pragma unroll
+      for (int h = hb; h < hb + dh; h++)
+#pragma unroll
+        for (int lo = 0; lo < L; lo++) {
+          const int x = h * L + lo, y = (h + dh) * L + lo;
+          pin2(wl[x], wh[x], wl[y], wh[y]);
+          wl[y] ^= wl[x];
+          wh[y] ^= wh[x];
+          gf16_muladd4(wl[x], wh[x], wl[y], wh[y], tb);
+          opaque(wl[x]);
+          opaque(wh[x]);
+          last = wh[x];
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // FFT, arrangement B
+#pragma unroll
+  for (int t = 0; (1 << t) < G; t++) {
+    const int dh = G >> (t + 1);
+#pragma unroll
+    for (int hb = 0; hb < G; hb += 2 * dh) {
+      const Perm16 tb = load_tab16(tw, S * hb + S * dh - 1, last);
+#pragma unroll
+      for (int h = hb; h < hb + dh; h++)
+#pragma unroll
+        for (int lo = 0; lo < L; lo++) {
+          const int x = h * L + lo, y = (h + dh) * L + lo;
+          pin2(wl[x], wh[x], wl[y], wh[y]);
+          gf16_muladd4(wl[x], wh[x], wl[y], wh[y], tb);
+          opaque(wl[x]);
+          opaque(wh[x]);
+          wl[y] ^= wl[x];
+          wh[y] ^= wh[x];
+          opaque(wl[y]);
+          opaque(wh[y]);
+          last = wh[y];
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  exchange(false);
+  last = wh[S - 1];
+  // FFT, arrangement A
+#pragma unroll
+  for (int lg = LOGS - 1; lg >= 0; lg--) {
+    const int D = 1 << lg;
+#pragma unroll
+    for (int base = 0; base < S; base += 2 * D) {
+      const Perm16 t = load_tab16(tw, wv * S + base + D - 1, last);
+#pragma unroll
+      for (int j = 0; j < D; j++) {
+        pin2(wl[base + j], wh[base + j], wl[base + j + D], wh[base + j + D]);
+        gf16_muladd4(wl[base + j], wh[base + j], wl[base + j + D], wh[base + j + D], t);
+        opaque(wl[base + j]);
+        opaque(wh[base + j]);
+        wl[base + j + D] ^= wl[base + j];
+        wh[base + j + D] ^= wh[base + j];
+        opaque(wl[base + j + D]);
+        opaque(wh[base + j + D]);
+        last = wh[base + j + D];
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(
+      g.out + (uint64_t)blockIdx.z * g.out_sq + (uint64_t)blockIdx.x * g.out_axis, 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < S; i++) {
+    const uint32_t so = (uint32_t)(wv * S + i) * out_shard;
+    __builtin_amdgcn_raw_buffer_store_b32(wl[i], rout, col, so, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(wh[i], rout, col + 32, so, 0);
+  }
+}
+
+template <int LOGK>
+static hipError_t launch_gf16p(const RsGeom& g, const DeviceTables& t, hipStream_t s) {
+  constexpr int K = 1 << LOGK;
+  constexpr int threads = 64 * (K / 32);
+  const size_t lds = (size_t)K * 64 * 4;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_rs_encode_gf16p<LOGK>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  dim3 grid(g.axes, (g.len + 511) / 512, g.nsq);
+  hipLaunchKernelGGL(k_rs_encode_gf16p<LOGK>, grid, dim3(threads), lds, s, g, t.tw16);
+  return hipGetLastError();
 }
 
 // ------------------------------------------------- LDS transform kernels
@@ -433,6 +709,12 @@ hipError_t launch_rs_encode(const RsGeom& g, const DeviceTables& t, hipStream_t 
     }
   } else {
     if (g.n > kMaxGf16Width) return hipErrorInvalidValue;
+    static const bool lds_only = [] {
+      const char* e = getenv("CEL_GF16_IMPL");  // "lds": force the LDS/gather kernel (A/B runs)
+      return e && std::string(e) == "lds";
+    }();
+    if (!lds_only && g.n == 256 && g.len % 512 == 0) return launch_gf16p<8>(g, t, s);
+    if (!lds_only && g.n == 512 && g.len % 512 == 0) return launch_gf16p<9>(g, t, s);
     dim3 grid(g.axes, g.len / 64, g.nsq);
     const size_t lds = (size_t)g.n * 64;
     if (lds > 64 * 1024)

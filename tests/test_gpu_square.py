@@ -102,3 +102,16 @@ def test_gf16_square_k256(ctx, oracle):
     assert np.array_equal(dev.cells, eds)
     assert np.array_equal(dev._row_roots, rr) and np.array_equal(dev._col_roots, cr)
     assert dev._dah == dah
+
+
+def test_gf16_square_k512(ctx, oracle):
+    """k = 512 (config 3's square, here on one GPU): GF(2^16) register kernel, 2k = 1024
+    trees. Roots, DAH and the EDS bytes (by digest) against the oracle restatement."""
+    import hashlib
+    k = 512
+    ods = random_ods(k, 512)
+    dev = run_device(ctx, ods)
+    eds, rr, cr, dah = oracle.extend_and_commit(ods)
+    assert hashlib.sha256(dev.cells.tobytes()).digest() == hashlib.sha256(eds.tobytes()).digest()
+    assert np.array_equal(dev._row_roots, rr) and np.array_equal(dev._col_roots, cr)
+    assert dev._dah == dah
