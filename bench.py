@@ -43,11 +43,197 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--phase-reps", type=int, default=10)
+    ap.add_argument("--mode", default="batch", choices=["batch", "sharded", "repair"],
+                    help="batch: independent squares per GPU (configs 2, 4); sharded: one square "
+                         "row-sharded over the ranks (config 3); repair: rsmt2d Repair (config 5)")
+    ap.add_argument("--repair-p", type=float, default=0.55, help="repair mode: cell survival probability")
     return ap.parse_args()
+
+
+def _cpu_cores():
+    cores = os.cpu_count() or 1
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        pass
+    # the GPU box grants a CPU share (OMP_NUM_THREADS) far below the visible core count
+    return min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+
+
+def run_sharded(a):
+    """Config 3: one k x k square per step, row-sharded over all ranks (strong scaling).
+    Rank r row-encodes k/N rows straight into the all-to-all layout, one RCCL
+    all_to_all_single transposes them into column slabs, each rank column-encodes and
+    hashes its slab, two all-gathers of 96-byte records and a combine give the roots
+    and the DAH on every rank. At N = 1 the same schedule runs without collectives."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    from celestia_eds import default_context
+    from celestia_eds.sharded import DeviceSteps, LocalComm, ShardedSquare, TorchComm
+    from celestia_eds.testfactory import random_ods
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    k = a.k
+    ctx = default_context(local)
+    steps = DeviceSteps(ctx, local)
+    sq = ShardedSquare(k, rank, world, steps)
+    ods = random_ods(k, 512)
+    lo, hi = sq.row_range()
+    sq.ods_rows.copy_(torch.from_numpy(np.ascontiguousarray(ods[lo:hi])))
+    comm = TorchComm() if dist is not None else None
+
+    def step():
+        if comm is not None:
+            sq.run(comm)
+        else:
+            LocalComm.run([sq])
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    sq.check_status()
+    # rank-local phase timing (HIP events on the launch stream = torch's current stream)
+    cur = torch.cuda.current_stream(dev)
+
+    def timed(fn, reps):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        fn()
+        e0.record(cur)
+        for _ in range(reps):
+            fn()
+        e1.record(cur)
+        e1.synchronize()
+        return e0.elapsed_time(e1) / reps / 1e3
+
+    t_rows = timed(sq.phase_rows, a.phase_reps)
+    t_cols = timed(sq.phase_cols, a.phase_reps)
+    value = a.steps / elapsed
+    rows_bytes = 1024 * k * k // world  # read k/N ODS rows + write their k parity shards
+    result = {
+        "metric": "EDS+DAH squares/sec (k=%d, row-sharded)" % k,
+        "value": value,
+        "unit": "squares/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": elapsed / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (testfactory-style sorted random namespaced shares)",
+        "ods_gbps": value * 512 * k * k / 1e9,
+        "config": {
+            "workload": f"k={k} ODS -> EDS + 4k NMT roots + DAH, one square row-sharded over {world} GPU(s)",
+            "k": k,
+            "share_size": 512,
+            "field": "GF(2^16)",
+            "parallelism": f"rowshard{world}",
+            "collectives": "all_to_all_single (data), all_gather x2 + all_reduce (records)" if world > 1
+            else "none (N=1)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "k_rs_encode_gf16p (row pass of this rank)",
+            "achieved": rows_bytes / t_rows / 1e9,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": rows_bytes / t_rows / 1e9 / HBM_PEAK_GBS,
+            "traffic": None,
+            "avg_launch_us": t_rows * 1e6,
+        },
+        "phase_us": {"rows": t_rows * 1e6, "cols_and_commit": t_cols * 1e6},
+    }
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def run_repair(a):
+    """Config 5: rsmt2d Repair of a k x k EDS from a random sample (cells kept with
+    probability --repair-p, seed 7): crossword erasure decode on the device, re-encode
+    check and root re-verification. Host-resident EDS in and out (the cel_repair
+    boundary), so the number includes the PCIe copies. Single rank."""
+    torch.cuda.set_device(0)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from celestia_eds import default_context
+    from celestia_eds.rsmt2d import ExtendedDataSquare
+    from celestia_eds.testfactory import random_ods
+    oracle.set_simd(True)
+    oracle.set_threads(_cpu_cores())
+    k, w = a.k, 2 * a.k
+    eds, rr, cr, _ = oracle.extend_and_commit(random_ods(k, 7))
+    present = (np.random.default_rng(7).random((w, w)) < a.repair_p).astype(np.uint8)
+    damaged = eds.copy()
+    damaged[present == 0] = 0
+    ctx = default_context(0)
+    rrl, crl = [r.tobytes() for r in rr], [c.tobytes() for c in cr]
+
+    def once():
+        sq = ExtendedDataSquare(damaged.copy(), ctx=ctx)
+        sq.Repair(rrl, crl, present=present.copy())
+        return sq
+
+    for _ in range(a.warmup):
+        once()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        sq = once()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    assert np.array_equal(sq.cells, eds), "repaired EDS differs"
+    n_cpu, t_cpu = 0, 0.0
+    while t_cpu < min(a.cpu_seconds, 10.0) and n_cpu < 20:
+        t1 = time.perf_counter()
+        rc, fixed, _, _ = oracle.repair(damaged, present, rr, cr)
+        t_cpu += time.perf_counter() - t1
+        n_cpu += 1
+        assert rc == 0 and np.array_equal(fixed, eds)
+    value = a.steps / elapsed
+    print(json.dumps({
+        "metric": "rsmt2d Repair squares/sec (k=%d, p=%.2f)" % (k, a.repair_p),
+        "value": value, "unit": "squares/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8", "data": "synthetic (testfactory-style ODS, random survival mask)",
+        "config": {"workload": f"Repair k={k} EDS from {present.mean():.3f} of its cells (host buffers, PCIe "
+                               f"included)", "k": k, "parallelism": "single"},
+        "cpu_baseline": {"value": n_cpu / t_cpu, "unit": "squares/s", "cores": oracle.lib().orc_get_threads(),
+                         "kind": "port", "sample": f"{n_cpu} repairs of the same damaged square (C restatement)"},
+    }), flush=True)
 
 
 def main():
     a = parse()
+    if a.mode == "sharded":
+        return run_sharded(a)
+    if a.mode == "repair":
+        return run_repair(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -166,14 +352,7 @@ def main():
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
         oracle.set_simd(True)
-        cores = os.cpu_count() or 1
-        try:
-            cores = len(os.sched_getaffinity(0))
-        except AttributeError:
-            pass
-        # the GPU box grants a CPU share (OMP_NUM_THREADS) far below the visible core count
-        cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
-        oracle.set_threads(cores)
+        oracle.set_threads(_cpu_cores())
         n_done, t_cpu = 0, 0.0
         dah_dev = sb.dah.cpu().numpy()
         parity = True

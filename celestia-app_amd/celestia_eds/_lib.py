@@ -26,7 +26,8 @@ EXPORTS = [
     "cel_extend_shares", "cel_extend_batch", "cel_dev_workspace_size", "cel_dev_extend_batch",
     "cel_dev_extend_only", "cel_dev_commit_only", "cel_codec_encode", "cel_codec_decode",
     "cel_codec_max_chunks", "cel_codec_name", "cel_codec_validate_chunk_size", "cel_axis_root",
-    "cel_nmt_root", "cel_dah_hash", "cel_repair",
+    "cel_nmt_root", "cel_dah_hash", "cel_repair", "cel_dev_shard_workspace_size", "cel_dev_shard_rows",
+    "cel_dev_shard_cols", "cel_dev_shard_finish",
 ]
 
 _lib = None
@@ -71,6 +72,10 @@ def load():
             "cel_nmt_root": (i32, [P, P, u32, u32, P, u32]),
             "cel_dah_hash": (i32, [P, P, P, u32, P]),
             "cel_repair": (i32, [P, P, P, u32, u32, P, P, P, P]),
+            "cel_dev_shard_workspace_size": (sz, [u32, u32]),
+            "cel_dev_shard_rows": (i32, [P, P, u32, u32, P, P]),
+            "cel_dev_shard_cols": (i32, [P, P, u32, u32, u32, P, P, P, P, P, u32]),
+            "cel_dev_shard_finish": (i32, [P, P, P, u32, u32, P, P, P, P, P, P, u32]),
         }
         for name, (res, args) in sigs.items():
             fn = getattr(l, name)

@@ -1,0 +1,179 @@
+"""Row-sharded extension of one square over several GPUs (config 3).
+
+One process per GPU. Rank r owns ODS rows [r*k/N, (r+1)*k/N) and, after one
+all-to-all transpose, EDS columns [r*w, (r+1)*w) with w = 2k/N:
+
+  1. rows    row-encode the local rows straight into the all-to-all send layout
+             [N][k/N][w][512] (block h = the cells of rank h's columns)
+  2. a2a     all_to_all_single: the received blocks, in rank order, are the top half
+             (rows 0..k-1) of this rank's column slab [2k][w][512]
+  3. cols    column-encode the slab (rows k..2k-1), hash its leaves once, build its
+             w column trees and the 2k row subtrees over its w columns
+  4. gather  all_gather the row-subtree records and the column-root records, and a
+             max all_reduce of the push-order status
+  5. finish  combine the N subtree roots of every row (log2 N levels of HashNode),
+             then DataAvailabilityHeader.Hash over rowRoots || colRoots
+
+The result is what da.ExtendShares + da.NewDataAvailabilityHeader
+(pkg/da/data_availability_header.go:65-75, :44-63) give for the whole square. The
+only data-path collective is the all-to-all (2k*k*512/N^2 bytes per peer); the
+gathers move 96-byte records. `steps` does the per-rank device work (DeviceSteps:
+the C ABI cel_dev_shard_*); `comm` the collectives (TorchComm: torch.distributed,
+i.e. RCCL over xGMI on the GPU box, gloo in the CPU tests).
+"""
+import ctypes
+
+from . import _lib
+
+RECORD = 96  # 90-byte NMT node + 6 zero bytes (CEL_NODE_RECORD)
+
+
+class TorchComm:
+    """Collectives over torch.distributed (backend "nccl" = RCCL, or "gloo")."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+
+    def all_to_all(self, out, inp):
+        self.dist.all_to_all_single(out, inp, group=self.group)
+
+    def all_gather(self, out, inp):
+        self.dist.all_gather_into_tensor(out, inp, group=self.group)
+
+    def all_reduce_max(self, t):
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
+
+
+class DeviceSteps:
+    """Per-rank device steps through the C ABI (device tensors, current HIP stream)."""
+
+    def __init__(self, ctx=None, device=0, order_check=True):
+        import torch
+        self.torch = torch
+        self.dev = torch.device("cuda", device)
+        self.ctx = ctx or _lib.default_context(device)
+        self.flags = _lib.FLAG_ORDER_CHECK if order_check else 0
+        self._work = None
+
+    def empty(self, shape, dtype):
+        return self.torch.empty(shape, dtype=dtype, device=self.dev)
+
+    @staticmethod
+    def _p(t):
+        return ctypes.c_void_p(t.data_ptr())
+
+    def _stream(self):
+        return ctypes.c_void_p(self.torch.cuda.current_stream(self.dev).cuda_stream)
+
+    def work(self, k, n):
+        size = self.ctx.lib.cel_dev_shard_workspace_size(k, n)
+        if self._work is None or self._work.numel() < size:
+            self._work = self.empty((size,), self.torch.uint8)
+        return self._work
+
+    def rows(self, ods_rows, k, n, send):
+        c = self.ctx
+        c.check(c.lib.cel_dev_shard_rows(c.handle, self._p(ods_rows), k, n, self._p(send), self._stream()))
+
+    def cols(self, slab, k, n, rank, col_rec, row_sub, status):
+        c = self.ctx
+        c.check(c.lib.cel_dev_shard_cols(c.handle, self._p(slab), k, n, rank, self._p(col_rec), self._p(row_sub),
+                                         self._p(status), self._p(self.work(k, n)), self._stream(), self.flags))
+
+    def finish(self, row_sub_all, col_rec_all, k, n, row_roots, col_roots, dah, status):
+        c = self.ctx
+        c.check(c.lib.cel_dev_shard_finish(c.handle, self._p(row_sub_all), self._p(col_rec_all), k, n,
+                                           self._p(row_roots), self._p(col_roots), self._p(dah), self._p(status),
+                                           self._p(self.work(k, n)), self._stream(), self.flags))
+
+
+class ShardedSquare:
+    """Buffers and phases of one rank of a row-sharded square of width k over n ranks."""
+
+    def __init__(self, k, rank, n, steps):
+        import torch
+        if n < 1 or (n & (n - 1)) or n > k:
+            raise ValueError(f"world size must be a power of two <= k: got {n}")
+        self.k, self.rank, self.n, self.steps = k, rank, n, steps
+        self.rows_per_rank, self.w = k // n, 2 * k // n
+        u8, i32 = torch.uint8, torch.int32
+        S, W = _lib.SHARE_SIZE, 2 * k
+        e = steps.empty
+        self.ods_rows = e((self.rows_per_rank, k, S), u8)
+        self.send = e((n, self.rows_per_rank, self.w, S), u8)
+        self.slab = e((W, self.w, S), u8)
+        self.col_rec = e((self.w, RECORD), u8)
+        self.row_sub = e((W, RECORD), u8)
+        self.row_sub_all = e((n, W, RECORD), u8)
+        self.col_rec_all = e((W, RECORD), u8)
+        self.status = e((1,), i32)
+        self.row_roots = e((W, _lib.NMT_NODE_SIZE), u8)
+        self.col_roots = e((W, _lib.NMT_NODE_SIZE), u8)
+        self.dah = e((32,), u8)
+
+    def row_range(self):
+        return self.rank * self.rows_per_rank, (self.rank + 1) * self.rows_per_rank
+
+    # -- phases (a driver may interleave them across simulated ranks)
+    def phase_rows(self):
+        self.steps.rows(self.ods_rows, self.k, self.n, self.send)
+
+    def exchange(self, comm):
+        top = self.slab[: self.k].view(self.n, self.rows_per_rank, self.w, _lib.SHARE_SIZE)
+        comm.all_to_all(top.view(-1), self.send.view(-1))
+
+    def phase_cols(self):
+        self.steps.cols(self.slab, self.k, self.n, self.rank, self.col_rec, self.row_sub, self.status)
+
+    def gather(self, comm):
+        comm.all_gather(self.row_sub_all.view(-1), self.row_sub.view(-1))
+        comm.all_gather(self.col_rec_all.view(-1), self.col_rec.view(-1))
+        comm.all_reduce_max(self.status)
+
+    def phase_finish(self):
+        self.steps.finish(self.row_sub_all, self.col_rec_all, self.k, self.n, self.row_roots, self.col_roots,
+                          self.dah, self.status)
+
+    def run(self, comm):
+        self.phase_rows()
+        self.exchange(comm)
+        self.phase_cols()
+        self.gather(comm)
+        self.phase_finish()
+        return self
+
+    def check_status(self):
+        st = int(self.status.cpu().item())
+        if st:
+            raise _lib.CelError(st, "invalid push order: leaf namespaces must be non-decreasing")
+
+
+class LocalComm:
+    """Collectives among ShardedSquare objects of one process (single-GPU rehearsal of
+    the N-rank schedule: same buffers, same layouts, copies instead of RCCL)."""
+
+    @staticmethod
+    def run(squares):
+        import torch
+        n = len(squares)
+        for s in squares:
+            s.phase_rows()
+        for h, dst in enumerate(squares):  # block h of every sender -> receiver h, sender order
+            top = dst.slab[: dst.k].view(n, dst.rows_per_rank, dst.w, _lib.SHARE_SIZE)
+            for r, src in enumerate(squares):
+                top[r].copy_(src.send[h])
+        for s in squares:
+            s.phase_cols()
+        row_sub_all = torch.stack([s.row_sub for s in squares])
+        col_rec_all = torch.cat([s.col_rec for s in squares])
+        status = torch.stack([s.status for s in squares]).max().reshape(1)
+        for s in squares:
+            s.row_sub_all.copy_(row_sub_all)
+            s.col_rec_all.copy_(col_rec_all)
+            s.status.copy_(status)
+            s.phase_finish()
+        return squares

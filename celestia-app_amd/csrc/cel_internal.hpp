@@ -31,6 +31,12 @@ struct RsGeom {
   // has them in registers): dcopy + s*dc_sq + a*dc_axis + i*dc_shard. nullptr = none.
   uint8_t* dcopy;
   uint64_t dc_sq, dc_axis, dc_shard;
+  // Blocked shard placement (row-sharded mode: the row pass writes straight into the
+  // all-to-all send layout). When blk_log != 0, output / dcopy shard j goes to
+  //   ((j >> blk_log) * *_blk) + (j & ((1 << blk_log) - 1)) * *_shard
+  // instead of j * *_shard. Only the GF(2^16) register kernel supports it.
+  uint32_t blk_log;
+  uint64_t out_blk, dc_blk;
   uint32_t n;     // data shards per axis (power of two)
   uint32_t len;   // bytes per shard (multiple of 64)
   uint32_t axes;  // axes per square
@@ -76,6 +82,15 @@ size_t nmt_root_workspace_size(uint32_t n);
 hipError_t launch_merkle_root(const uint8_t* items, uint32_t n, uint32_t item_len, uint8_t* out,
                               void* work, hipStream_t s);
 size_t merkle_workspace_size(uint32_t n);
+
+// Row-sharded mode (one column slab of one square per rank).
+size_t slab_workspace_size(uint32_t k, uint32_t w);
+hipError_t launch_slab_commit(const uint8_t* slab, uint32_t k, uint32_t c0, uint32_t w, uint32_t* col_rec,
+                              uint32_t* row_sub, int32_t* status, void* work, bool order_check, hipStream_t s);
+size_t shard_finish_workspace_size(uint32_t k, uint32_t nranks);
+hipError_t launch_shard_finish(const uint32_t* row_subs, const uint32_t* col_rec, uint32_t k, uint32_t nranks,
+                               uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah, int32_t* status, void* work,
+                               bool order_check, hipStream_t s);
 
 // Repair helpers (repair_kernels.hip, nmt_kernels.hip).
 hipError_t launch_gather_axes(const uint8_t* eds, const uint8_t* mask, uint32_t W, const int32_t* idx, int is_col,

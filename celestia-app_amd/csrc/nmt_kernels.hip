@@ -156,24 +156,11 @@ __device__ __forceinline__ bool ns_less(const uint32_t* __restrict__ a, const ui
   return res < 0;
 }
 
-// grid: x = cell block (256 cells), y = square. Writes leaf nodes [sq][W*W][24].
-template <bool ORDER>
-__global__ CEL_LEAF_BOUNDS void k_leaf(const uint8_t* __restrict__ eds, uint32_t k, uint32_t* __restrict__ leaves,
-                                              int32_t* __restrict__ bad_axis) {
-  const uint32_t W = 2 * k;
-  const uint32_t cell = blockIdx.x * 256u + threadIdx.x;
-  if (cell >= W * W) return;
-  const uint32_t r = cell / W, c = cell % W;
-  const uint64_t sq_eds = (uint64_t)W * W * kShare;
-  const uint32_t* sh = reinterpret_cast<const uint32_t*>(eds + blockIdx.y * sq_eds + (uint64_t)cell * kShare);
-  const bool q0 = (r < k) && (c < k);
-  if (ORDER && q0) {
-    if (c > 0 && ns_less(sh, sh - kShare / 4)) atomicMin(bad_axis + blockIdx.y, (int32_t)r);
-    if (r > 0 && ns_less(sh, sh - (uint64_t)W * kShare / 4)) atomicMin(bad_axis + blockIdx.y, (int32_t)(W + c));
-  }
+// Leaf node of one EDS cell: ns || ns || SHA256(0x00 || ns || share), ns = share[0:29]
+// for Q0 cells and 0xFF*29 (parity namespace) otherwise.
+__device__ __forceinline__ void make_leaf_node(const uint32_t* __restrict__ sh, bool q0, uint32_t (&nd)[kNodeWords]) {
   uint32_t st[8];
   leaf_hash(st, sh, q0);
-  uint32_t nd[kNodeWords];
   if (q0) {
     const uint4* p4 = reinterpret_cast<const uint4*>(sh);
     uint32_t s[8];
@@ -191,6 +178,25 @@ __global__ CEL_LEAF_BOUNDS void k_leaf(const uint8_t* __restrict__ eds, uint32_t
     nd[14] = 0xFFFFu;
   }
   put_digest(nd, st);
+}
+
+// grid: x = cell block (256 cells), y = square. Writes leaf nodes [sq][W*W][24].
+template <bool ORDER>
+__global__ CEL_LEAF_BOUNDS void k_leaf(const uint8_t* __restrict__ eds, uint32_t k, uint32_t* __restrict__ leaves,
+                                              int32_t* __restrict__ bad_axis) {
+  const uint32_t W = 2 * k;
+  const uint32_t cell = blockIdx.x * 256u + threadIdx.x;
+  if (cell >= W * W) return;
+  const uint32_t r = cell / W, c = cell % W;
+  const uint64_t sq_eds = (uint64_t)W * W * kShare;
+  const uint32_t* sh = reinterpret_cast<const uint32_t*>(eds + blockIdx.y * sq_eds + (uint64_t)cell * kShare);
+  const bool q0 = (r < k) && (c < k);
+  if (ORDER && q0) {
+    if (c > 0 && ns_less(sh, sh - kShare / 4)) atomicMin(bad_axis + blockIdx.y, (int32_t)r);
+    if (r > 0 && ns_less(sh, sh - (uint64_t)W * kShare / 4)) atomicMin(bad_axis + blockIdx.y, (int32_t)(W + c));
+  }
+  uint32_t nd[kNodeWords];
+  make_leaf_node(sh, q0, nd);
   store_node(leaves + ((uint64_t)blockIdx.y * W * W + cell) * kNodeWords, nd);
 }
 
@@ -454,6 +460,170 @@ hipError_t launch_commit(const uint8_t* eds, uint32_t k, uint32_t nsq, uint8_t* 
   }
   const size_t lds = (size_t)trees * 8 * 4;
   hipLaunchKernelGGL(k_merkle, dim3(nsq), dim3(256), lds, s, roots, leafd, trees, dah, row_roots, col_roots, bad, status);
+  return hipGetLastError();
+}
+
+
+// ------------------------------------------------------- row-sharded mode (§8e)
+//
+// A rank holds a column slab of one EDS: slab[i][j] = cell (i, c0 + j), i < 2k, j < w,
+// w = 2k / nranks. It hashes the slab's leaves once, builds its w column trees in full
+// and, for every row, the subtree root over its w-wide slice (an aligned power-of-two
+// range, hence a subtree of the row's perfect tree). Rank-ordered subtree roots are
+// combined into the row roots after an all-gather.
+
+template <bool ORDER>
+__global__ CEL_LEAF_BOUNDS void k_slab_leaf(const uint8_t* __restrict__ slab, uint32_t k, uint32_t c0, uint32_t w,
+                                            uint32_t* __restrict__ leaves, int32_t* __restrict__ bad_axis) {
+  const uint32_t W = 2 * k;
+  const uint32_t cell = blockIdx.x * 256u + threadIdx.x;
+  if (cell >= W * w) return;
+  const uint32_t i = cell / w, j = cell % w, c = c0 + j;
+  const uint32_t* sh = reinterpret_cast<const uint32_t*>(slab + (uint64_t)cell * kShare);
+  const bool q0 = (i < k) && (c < k);
+  if (ORDER && q0) {
+    if (j > 0 && ns_less(sh, sh - kShare / 4)) atomicMin(bad_axis, (int32_t)i);
+    if (i > 0 && ns_less(sh, sh - (uint64_t)w * kShare / 4)) atomicMin(bad_axis, (int32_t)(W + c));
+  }
+  uint32_t nd[kNodeWords];
+  make_leaf_node(sh, q0, nd);
+  store_node(leaves + (uint64_t)cell * kNodeWords, nd);
+}
+
+// First tree level over a strided node grid: tree t's leaf l is in[t * tstride + l * lstride].
+// Output compact: out[t][nin / 2].
+__global__ CEL_LEVEL_BOUNDS void k_level_grid(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint32_t nin,
+                                              uint32_t trees, uint32_t tstride, uint32_t lstride) {
+  const uint32_t nout = nin / 2;
+  const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
+  if (idx >= trees * nout) return;
+  const uint32_t t = idx / nout, j = idx % nout;
+  const uint64_t li = (uint64_t)t * tstride + (uint64_t)(2 * j) * lstride, ri = li + lstride;
+  uint32_t L[kNodeWords], R[kNodeWords], o[kNodeWords];
+  load_node(in + li * kNodeWords, L);
+  load_node(in + ri * kNodeWords, R);
+  hash_node(L, R, o);
+  store_node(out + (uint64_t)idx * kNodeWords, o);
+}
+
+// Push order across slab boundaries (rows of Q0): the last leaf of slab r-1 must not
+// carry a larger namespace than the first leaf of slab r. Within a sorted slab those are
+// the subtree's maxNs and minNs. subs: [nranks][2k] records.
+__global__ void k_slab_boundary(const uint32_t* __restrict__ subs, uint32_t k, uint32_t w, uint32_t nranks,
+                                int32_t* __restrict__ bad_axis) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= k) return;
+  const uint32_t W = 2 * k;
+  for (uint32_t r = 1; r < nranks && r * w < k; r++) {
+    const uint8_t* L = reinterpret_cast<const uint8_t*>(subs + ((uint64_t)(r - 1) * W + i) * kNodeWords);
+    const uint8_t* R = reinterpret_cast<const uint8_t*>(subs + ((uint64_t)r * W + i) * kNodeWords);
+    for (uint32_t b = 0; b < kNs; b++) {
+      const uint8_t lm = L[kNs + b], rm = R[b];
+      if (lm != rm) {
+        if (rm < lm) atomicMin(bad_axis, (int32_t)i);
+        break;
+      }
+    }
+  }
+}
+
+__global__ void k_status_from_bad(const int32_t* __restrict__ bad_axis, int32_t* __restrict__ status) {
+  if (threadIdx.x == 0 && *bad_axis != INT_MAX) *status = CEL_EORDER;
+}
+
+__global__ void k_pack_records(const uint32_t* __restrict__ rec, uint32_t n, uint8_t* __restrict__ out) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n * kNode) return;
+  out[b] = reinterpret_cast<const uint8_t*>(rec + (uint64_t)(b / kNode) * kNodeWords)[b % kNode];
+}
+
+// Reduce `trees` trees of nin nodes each (first level strided, then compact) to one
+// record per tree in `roots`. ping/pong hold trees * nin / 2 records each.
+static void reduce_grid(const uint32_t* in, uint32_t nin, uint32_t trees, uint32_t tstride, uint32_t lstride,
+                        uint32_t* ping, uint32_t* pong, uint32_t* roots, hipStream_t s) {
+  if (nin < 2) return;  // callers copy single-leaf trees themselves
+  uint32_t nout = nin / 2;
+  uint32_t* out = (nout == 1) ? roots : ping;
+  hipLaunchKernelGGL(k_level_grid, dim3((trees * nout + 255) / 256), dim3(256), 0, s, in, out, nin, trees, tstride,
+                     lstride);
+  const uint32_t* src = out;
+  uint32_t* dst = pong;
+  nin = nout;
+  while (nin > 1) {
+    nout = nin / 2;
+    out = (nout == 1) ? roots : dst;
+    hipLaunchKernelGGL(k_level<false>, dim3((trees * nout + 255) / 256, 1), dim3(256), 0, s, src, out, 0u, nin, trees,
+                       nullptr);
+    src = out;
+    dst = (dst == ping) ? pong : ping;
+    nin = nout;
+  }
+}
+
+// Workspace: leaves [2k*w] | ping [k*w] | pong [k*w] | bad int32
+size_t slab_workspace_size(uint32_t k, uint32_t w) {
+  const size_t nb = kNodeWords * 4, W = 2 * (size_t)k;
+  return align256(W * w * nb) + 2 * align256((size_t)k * w * nb + nb) + align256(W * 2 * nb) + 256;
+}
+
+hipError_t launch_slab_commit(const uint8_t* slab, uint32_t k, uint32_t c0, uint32_t w, uint32_t* col_rec,
+                              uint32_t* row_sub, int32_t* status, void* work, bool order_check, hipStream_t s) {
+  const uint32_t W = 2 * k;
+  const size_t nb = kNodeWords * 4;
+  uint8_t* base = static_cast<uint8_t*>(work);
+  uint32_t* leaves = reinterpret_cast<uint32_t*>(base);
+  base += align256((size_t)W * w * nb);
+  uint32_t* ping = reinterpret_cast<uint32_t*>(base);
+  base += align256((size_t)k * w * nb + nb);
+  uint32_t* pong = reinterpret_cast<uint32_t*>(base);
+  base += align256((size_t)k * w * nb + nb);
+  base += align256((size_t)W * 2 * nb);
+  int32_t* bad = reinterpret_cast<int32_t*>(base);
+  hipLaunchKernelGGL(k_fill_i32, dim3(1), dim3(64), 0, s, bad, 1u, INT_MAX);
+  hipLaunchKernelGGL(k_fill_i32, dim3(1), dim3(64), 0, s, status, 1u, 0);
+  dim3 gl((W * w + 255) / 256);
+  if (order_check) hipLaunchKernelGGL(k_slab_leaf<true>, gl, dim3(256), 0, s, slab, k, c0, w, leaves, bad);
+  else hipLaunchKernelGGL(k_slab_leaf<false>, gl, dim3(256), 0, s, slab, k, c0, w, leaves, bad);
+  // w column trees of 2k leaves (leaf i of column j at i*w + j)
+  reduce_grid(leaves, W, w, 1, w, ping, pong, col_rec, s);
+  // 2k row subtrees of w leaves (leaf j of row i at i*w + j)
+  if (w == 1) (void)hipMemcpyAsync(row_sub, leaves, (size_t)W * nb, hipMemcpyDeviceToDevice, s);
+  else reduce_grid(leaves, w, W, w, 1, ping, pong, row_sub, s);
+  hipLaunchKernelGGL(k_status_from_bad, dim3(1), dim3(64), 0, s, bad, status);
+  return hipGetLastError();
+}
+
+// Workspace: ping/pong [2k * nranks / 2] | items [4k] | leafd unused | bad
+size_t shard_finish_workspace_size(uint32_t k, uint32_t nranks) {
+  const size_t nb = kNodeWords * 4, W = 2 * (size_t)k;
+  return 2 * align256(W * (nranks / 2 + 1) * nb) + align256(2 * W * nb) + 256;
+}
+
+hipError_t launch_shard_finish(const uint32_t* row_subs, const uint32_t* col_rec, uint32_t k, uint32_t nranks,
+                               uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah, int32_t* status, void* work,
+                               bool order_check, hipStream_t s) {
+  const uint32_t W = 2 * k, w = W / nranks;
+  const size_t nb = kNodeWords * 4;
+  uint8_t* base = static_cast<uint8_t*>(work);
+  uint32_t* ping = reinterpret_cast<uint32_t*>(base);
+  base += align256((size_t)W * (nranks / 2 + 1) * nb);
+  uint32_t* pong = reinterpret_cast<uint32_t*>(base);
+  base += align256((size_t)W * (nranks / 2 + 1) * nb);
+  uint32_t* items = reinterpret_cast<uint32_t*>(base);  // [rows 2k | cols 2k]
+  base += align256((size_t)2 * W * nb);
+  int32_t* bad = reinterpret_cast<int32_t*>(base);
+  hipLaunchKernelGGL(k_fill_i32, dim3(1), dim3(64), 0, s, bad, 1u, INT_MAX);
+  if (order_check && nranks > 1)
+    hipLaunchKernelGGL(k_slab_boundary, dim3((k + 255) / 256), dim3(256), 0, s, row_subs, k, w, nranks, bad);
+  // row i's subtree from rank r is row_subs[r][i]: trees of nranks leaves, stride W
+  if (nranks == 1) (void)hipMemcpyAsync(items, row_subs, (size_t)W * nb, hipMemcpyDeviceToDevice, s);
+  else reduce_grid(row_subs, nranks, W, 1, W, ping, pong, items, s);
+  (void)hipMemcpyAsync(items + (size_t)W * kNodeWords, col_rec, (size_t)W * nb, hipMemcpyDeviceToDevice, s);
+  // previous status (all-reduced over ranks by the caller) survives; boundary adds to it
+  hipLaunchKernelGGL(k_status_from_bad, dim3(1), dim3(64), 0, s, bad, status);
+  const size_t lds = (size_t)2 * W * 8 * 4;
+  hipLaunchKernelGGL(k_merkle, dim3(1), dim3(256), lds, s, items, nullptr, 2 * W, dah, row_roots, col_roots,
+                     nullptr, nullptr);
   return hipGetLastError();
 }
 

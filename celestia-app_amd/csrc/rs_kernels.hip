@@ -369,13 +369,17 @@ __global__ __launch_bounds__(64 * (1 << (LOGK - 5))) void k_rs_encode_gf16p(RsGe
     wl[i] = __builtin_amdgcn_raw_buffer_load_b32(rin, col, so, 0);
     wh[i] = __builtin_amdgcn_raw_buffer_load_b32(rin, col + 32, so, 0);
   }
+  // shard j -> byte offset, linear or blocked (see RsGeom::blk_log)
+  const uint32_t blk_mask = g.blk_log ? (1u << g.blk_log) - 1u : 0xFFFFFFFFu;
+  const uint32_t blk_shift = g.blk_log ? g.blk_log : 31u;
+  auto place = [&](uint32_t j, uint32_t shard, uint32_t blk) { return (j >> blk_shift) * blk + (j & blk_mask) * shard; };
   if (g.dcopy) {
     const __amdgpu_buffer_rsrc_t rdc = __builtin_amdgcn_make_buffer_rsrc(
         g.dcopy + (uint64_t)blockIdx.z * g.dc_sq + (uint64_t)blockIdx.x * g.dc_axis, 0, 0x7fffffff, 0x00020000);
-    const uint32_t dc_shard = (uint32_t)g.dc_shard;
+    const uint32_t dc_shard = (uint32_t)g.dc_shard, dc_blk = (uint32_t)g.dc_blk;
 #pragma unroll
     for (int i = 0; i < S; i++) {
-      const uint32_t so = (uint32_t)(wv * S + i) * dc_shard;
+      const uint32_t so = place((uint32_t)(wv * S + i), dc_shard, dc_blk);
       __builtin_amdgcn_raw_buffer_store_b32(wl[i], rdc, col, so, 0);
       __builtin_amdgcn_raw_buffer_store_b32(wh[i], rdc, col + 32, so, 0);
     }
@@ -500,9 +504,10 @@ __global__ __launch_bounds__(64 * (1 << (LOGK - 5))) void k_rs_encode_gf16p(RsGe
   }
   const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(
       g.out + (uint64_t)blockIdx.z * g.out_sq + (uint64_t)blockIdx.x * g.out_axis, 0, 0x7fffffff, 0x00020000);
+  const uint32_t out_blk = (uint32_t)g.out_blk;
 #pragma unroll
   for (int i = 0; i < S; i++) {
-    const uint32_t so = (uint32_t)(wv * S + i) * out_shard;
+    const uint32_t so = place((uint32_t)(wv * S + i), out_shard, out_blk);
     __builtin_amdgcn_raw_buffer_store_b32(wl[i], rout, col, so, 0);
     __builtin_amdgcn_raw_buffer_store_b32(wh[i], rout, col + 32, so, 0);
   }
@@ -694,6 +699,7 @@ static bool use_perm_gf8(uint32_t n) {
 
 hipError_t launch_rs_encode(const RsGeom& g, const DeviceTables& t, hipStream_t s) {
   if (g.axes == 0 || g.nsq == 0) return hipSuccess;
+  if (g.blk_log && !((g.n == 256 || g.n == 512) && g.len % 512 == 0)) return hipErrorInvalidValue;
   if (2 * g.n <= 256 && !use_perm_gf8(g.n) && g.len % 32 == 0) return launch_rs_encode_bitslice(g, s);
   if (2 * g.n <= 256) {
     switch (g.n) {
@@ -713,8 +719,9 @@ hipError_t launch_rs_encode(const RsGeom& g, const DeviceTables& t, hipStream_t 
       const char* e = getenv("CEL_GF16_IMPL");  // "lds": force the LDS/gather kernel (A/B runs)
       return e && std::string(e) == "lds";
     }();
-    if (!lds_only && g.n == 256 && g.len % 512 == 0) return launch_gf16p<8>(g, t, s);
-    if (!lds_only && g.n == 512 && g.len % 512 == 0) return launch_gf16p<9>(g, t, s);
+    const bool reg = !lds_only || g.blk_log;
+    if (reg && g.n == 256 && g.len % 512 == 0) return launch_gf16p<8>(g, t, s);
+    if (reg && g.n == 512 && g.len % 512 == 0) return launch_gf16p<9>(g, t, s);
     dim3 grid(g.axes, g.len / 64, g.nsq);
     const size_t lds = (size_t)g.n * 64;
     if (lds > 64 * 1024)

@@ -106,6 +106,39 @@ cel_status cel_dev_commit_only(cel_ctx* ctx, const void* d_eds, uint32_t n, uint
                                void* d_row_roots, void* d_col_roots, void* d_dah,
                                int32_t* d_status, void* d_work, void* stream, uint32_t flags);
 
+/* ------------------------------------------- row-sharded square (multi-GPU)
+ * One square extended by nranks processes, one per GPU (config 3).
+ * Replaces, for a square too large for one device's share of the work, the same
+ * da.ExtendShares + NewDataAvailabilityHeader pair (data_availability_header.go:65-75,
+ * :44-63). Rank r owns ODS rows [r*k/nranks, (r+1)*k/nranks) and, after the column
+ * transpose, EDS columns [r*w, (r+1)*w) with w = 2k/nranks. The collectives (one
+ * all-to-all, two all-gathers, one max-all-reduce of the status) belong to the caller
+ * (RCCL through torch.distributed); these calls are the per-rank device steps.
+ * Supported for k in {256, 512} (Leopard GF(2^16)), nranks a power of two <= k.
+ * Node records are 96 bytes: the 90-byte NMT node and 6 zero bytes. */
+#define CEL_NODE_RECORD 96u
+size_t cel_dev_shard_workspace_size(uint32_t k, uint32_t nranks);
+/* Step 1: row-encode this rank's k/nranks ODS rows (d_ods_rows: [k/nranks][k][512])
+ * straight into the all-to-all send buffer d_send: [nranks][k/nranks][w][512]
+ * (block h = the cells of columns [h*w, (h+1)*w), Q0 and Q1 alike). */
+cel_status cel_dev_shard_rows(cel_ctx* ctx, const void* d_ods_rows, uint32_t k, uint32_t nranks, void* d_send,
+                              void* stream);
+/* Step 2 (after the all-to-all into the top half of d_slab): d_slab is [2k][w][512]
+ * with rows [0, k) received in rank order. Column-encodes the slab in place (rows
+ * [k, 2k)), hashes its 2k*w leaves once, and writes the w column-root records
+ * (d_col_rec: [w][96]) and the 2k row-subtree records over this slab's columns
+ * (d_row_sub: [2k][96]). *d_status = 0 or CEL_EORDER (within-slab push order). */
+cel_status cel_dev_shard_cols(cel_ctx* ctx, void* d_slab, uint32_t k, uint32_t nranks, uint32_t rank,
+                              void* d_col_rec, void* d_row_sub, int32_t* d_status, void* d_work, void* stream,
+                              uint32_t flags);
+/* Step 3 (after all-gathering the records of every rank, rank order):
+ * d_row_sub_all [nranks][2k][96], d_col_rec_all [2k][96] -> d_row_roots, d_col_roots
+ * (2k x 90 B each) and d_dah (32 B). *d_status (in: max over ranks of step 2) gains
+ * CEL_EORDER if the push order breaks across slab boundaries. */
+cel_status cel_dev_shard_finish(cel_ctx* ctx, const void* d_row_sub_all, const void* d_col_rec_all, uint32_t k,
+                                uint32_t nranks, void* d_row_roots, void* d_col_roots, void* d_dah,
+                                int32_t* d_status, void* d_work, void* stream, uint32_t flags);
+
 /* ------------------------------------------------------ rsmt2d.Codec surface
  * Leopard RS (klauspost/reedsolomon v1.12.1 New(n, n, WithLeopardGF(true))):
  * GF(2^8) when 2n <= 256, GF(2^16) otherwise. len must be a positive multiple
