@@ -114,8 +114,8 @@ def run_sharded(a):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     sq.check_status()
-    # rank-local phase timing (HIP events on the launch stream = torch's current stream)
-    cur = torch.cuda.current_stream(dev)
+    # rank-local phase timing (HIP events on the launch stream of the device steps)
+    cur = steps.stream
 
     def timed(fn, reps):
         e0 = torch.cuda.Event(enable_timing=True)
@@ -128,8 +128,9 @@ def run_sharded(a):
         e1.synchronize()
         return e0.elapsed_time(e1) / reps / 1e3
 
-    t_rows = timed(sq.phase_rows, a.phase_reps)
-    t_cols = timed(sq.phase_cols, a.phase_reps)
+    with sq.scope():
+        t_rows = timed(sq.phase_rows, a.phase_reps)
+        t_cols = timed(sq.phase_cols, a.phase_reps)
     value = a.steps / elapsed
     rows_bytes = 1024 * k * k // world  # read k/N ODS rows + write their k parity shards
     result = {

@@ -21,6 +21,7 @@ gathers move 96-byte records. `steps` does the per-rank device work (DeviceSteps
 the C ABI cel_dev_shard_*); `comm` the collectives (TorchComm: torch.distributed,
 i.e. RCCL over xGMI on the GPU box, gloo in the CPU tests).
 """
+import contextlib
 import ctypes
 
 from . import _lib
@@ -58,6 +59,13 @@ class DeviceSteps:
         self.ctx = ctx or _lib.default_context(device)
         self.flags = _lib.FLAG_ORDER_CHECK if order_check else 0
         self._work = None
+        # A dedicated (non-null) stream: the C ABI maps a NULL stream to the ctx's own
+        # stream, so torch's legacy default stream cannot be used to order the kernels
+        # with torch copies and collectives. Drivers enter scope() around every phase.
+        self.stream = torch.cuda.Stream(device=self.dev)
+
+    def scope(self):
+        return self.torch.cuda.stream(self.stream)
 
     def empty(self, shape, dtype):
         return self.torch.empty(shape, dtype=dtype, device=self.dev)
@@ -67,7 +75,7 @@ class DeviceSteps:
         return ctypes.c_void_p(t.data_ptr())
 
     def _stream(self):
-        return ctypes.c_void_p(self.torch.cuda.current_stream(self.dev).cuda_stream)
+        return ctypes.c_void_p(self.stream.cuda_stream)
 
     def work(self, k, n):
         size = self.ctx.lib.cel_dev_shard_workspace_size(k, n)
@@ -138,12 +146,17 @@ class ShardedSquare:
         self.steps.finish(self.row_sub_all, self.col_rec_all, self.k, self.n, self.row_roots, self.col_roots,
                           self.dah, self.status)
 
+    def scope(self):
+        sc = getattr(self.steps, "scope", None)
+        return sc() if sc else contextlib.nullcontext()
+
     def run(self, comm):
-        self.phase_rows()
-        self.exchange(comm)
-        self.phase_cols()
-        self.gather(comm)
-        self.phase_finish()
+        with self.scope():
+            self.phase_rows()
+            self.exchange(comm)
+            self.phase_cols()
+            self.gather(comm)
+            self.phase_finish()
         return self
 
     def check_status(self):
@@ -158,6 +171,12 @@ class LocalComm:
 
     @staticmethod
     def run(squares):
+        import torch
+        with squares[0].scope():
+            return LocalComm._run(squares)
+
+    @staticmethod
+    def _run(squares):
         import torch
         n = len(squares)
         for s in squares:

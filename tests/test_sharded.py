@@ -90,7 +90,7 @@ def test_device_sharded_local(ctx, oracle, k, n):
         a, b = s.row_range()
         s.ods_rows.copy_(torch.from_numpy(np.ascontiguousarray(ods[a:b])))
     LocalComm.run(squares)
-    torch.cuda.synchronize()
+    steps.stream.synchronize()
     eds, rr, cr, dah = oracle.extend_and_commit(ods)
     w = 2 * k // n
     for r, s in enumerate(squares):
