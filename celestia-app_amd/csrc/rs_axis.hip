@@ -1,0 +1,223 @@
+// Leopard GF(2^8) encode, one wave per axis slice (k <= 128).
+//
+// Same transform as k_rs_encode_gf8 (SURVEY.md Appendix A.2 in radix-2 form, see the
+// header of rs_kernels.hip), laid out so that nothing is shared between waves:
+//   - a wave owns one tile = (square, axis, 256-byte slice); lane l holds dword l of
+//     the slice of every one of the K data shards of the axis in VGPRs (K <= 128);
+//   - every radix-2 layer is lane-local, so there is no LDS image and no barrier: the
+//     waves of a CU drift apart and one wave's loads and stores run under the
+//     butterflies of the others;
+//   - the skew index of every butterfly is a compile-time constant, so the v_perm
+//     product tables are immediates (no table loads), "multiply by zero" butterflies
+//     (skew == 255) lose their multiply and "multiply by one" becomes an xor.
+// Multiply: the byte splits into 3+3+2 bits, each looked up with one v_perm_b32 in
+// an 8/8/4-entry product table (as rs_kernels.hip gf8_mul4).
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+
+#include "cel_internal.hpp"
+#include "gf8_constexpr.hpp"
+
+namespace cel {
+namespace ax {
+
+using cx::add_mod8;
+using cx::kGf8;
+using cx::sfor;
+
+struct Tab {
+  uint32_t t0l, t0h, t1l, t1h, t2;
+};
+
+constexpr uint32_t cmul(uint32_t a, uint32_t lm) { return a == 0 ? 0u : kGf8.exp[add_mod8(kGf8.log[a], lm)]; }
+
+// Product tables of c = exp(lm): T0[n] = c*n, T1[n] = c*(n << 3) (n < 8), T2[n] = c*(n << 6) (n < 4).
+constexpr Tab make_tab(uint32_t lm) {
+  Tab t{0, 0, 0, 0, 0};
+  for (uint32_t n = 0; n < 4; n++) {
+    t.t0l |= cmul(n, lm) << (8 * n);
+    t.t0h |= cmul(n + 4, lm) << (8 * n);
+    t.t1l |= cmul(n << 3, lm) << (8 * n);
+    t.t1h |= cmul((n + 4) << 3, lm) << (8 * n);
+    t.t2 |= cmul(n << 6, lm) << (8 * n);
+  }
+  return t;
+}
+
+// Constants materialised where they are used (volatile asm: the compiler would
+// otherwise CSE the table constants of all twiddles into VGPRs live across the whole
+// transform). gfx950 VOP3 takes no literal and reads one SGPR, so each 8-entry
+// product table has one dword in an SGPR (s_mov on the scalar unit) and one in a VGPR.
+template <uint32_t C>
+__device__ __forceinline__ uint32_t sconst() {
+  uint32_t r;
+  asm volatile("s_mov_b32 %0, %1" : "=s"(r) : "i"(C));
+  return r;
+}
+template <uint32_t C>
+__device__ __forceinline__ uint32_t vconst() {
+  uint32_t r;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "i"(C));
+  return r;
+}
+
+// Multiplier by c = exp(LM), tables materialised once per butterfly group.
+// LM == 255 is the zero twiddle (nothing to add), c == 1 is a plain xor.
+template <uint32_t LM>
+struct Mul {
+  static constexpr bool kZero = LM == 255u;
+  static constexpr bool kOne = !kZero && cmul(1, LM) == 1u;
+  static constexpr Tab t = make_tab(kZero ? 0u : LM);
+  uint32_t t0l, t0h, t1l, t1h, t2;
+  __device__ __forceinline__ Mul() {
+    if constexpr (!kZero && !kOne) {
+      t0h = sconst<t.t0h>();
+      t1h = sconst<t.t1h>();
+      t2 = sconst<t.t2>();
+      t0l = vconst<t.t0l>();
+      t1l = vconst<t.t1l>();
+    }
+  }
+  // x ^= c * y on 4 bytes
+  __device__ __forceinline__ void muladd(uint32_t& x, uint32_t y) const {
+    if constexpr (kOne) {
+      x ^= y;
+    } else if constexpr (!kZero) {
+      const uint32_t s0 = y & 0x07070707u;
+      const uint32_t s1 = (y >> 3) & 0x07070707u;
+      const uint32_t s2 = (y >> 6) & 0x03030303u;
+      const uint32_t p0 = __builtin_amdgcn_perm(t0h, t0l, s0);
+      const uint32_t p1 = __builtin_amdgcn_perm(t1h, t1l, s1);
+      const uint32_t p2 = __builtin_amdgcn_perm(0u, t2, s2);
+      x = __builtin_amdgcn_bitop3_b32(x, p0, p1, 0x96) ^ p2;
+    }
+  }
+};
+
+// Pins a butterfly's pair (asm volatile keeps the order): stops the combiner from
+// folding xor chains across butterflies, which keeps extra values alive and spills.
+__device__ __forceinline__ void pin(uint32_t& a, uint32_t& b) { asm volatile("" : "+v"(a), "+v"(b)); }
+
+// Leopard IFFT over the data coset (offset K) then FFT over the parity coset (offset 0),
+// radix 2, all K shards in w[]. Skew index: IFFT K-1 + base + D, FFT base + D - 1.
+template <int K>
+__device__ __forceinline__ void transform(uint32_t (&w)[K]) {
+  constexpr int LOGK = __builtin_ctz(K);
+  sfor<LOGK>([&](auto lg) {
+    constexpr int D = 1 << decltype(lg)::value;
+    sfor<K / (2 * D)>([&](auto bi) {
+      constexpr int base = decltype(bi)::value * 2 * D;
+      const Mul<kGf8.skew[K - 1 + base + D]> m;
+      sfor<D>([&](auto j) {
+        constexpr int a = base + decltype(j)::value;
+        pin(w[a], w[a + D]);
+        w[a + D] ^= w[a];
+        m.muladd(w[a], w[a + D]);
+        pin(w[a], w[a + D]);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    });
+  });
+  sfor<LOGK>([&](auto t) {
+    constexpr int D = K >> (decltype(t)::value + 1);
+    sfor<K / (2 * D)>([&](auto bi) {
+      constexpr int base = decltype(bi)::value * 2 * D;
+      const Mul<kGf8.skew[base + D - 1]> m;
+      sfor<D>([&](auto j) {
+        constexpr int a = base + decltype(j)::value;
+        pin(w[a], w[a + D]);
+        m.muladd(w[a], w[a + D]);
+        w[a + D] ^= w[a];
+        pin(w[a], w[a + D]);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    });
+  });
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+
+// DBG (profiling only, CEL_RS_DEBUG): 1 = loads and stores without the transform,
+// 2 = the transform without global memory traffic.
+template <int LOGK, int DBG>
+__global__ __launch_bounds__(256, 3) void k_rs_axis_gf8(RsGeom g, uint32_t nslice, uint32_t ntiles) {
+  constexpr int K = 1 << LOGK;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t tile = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+  if (tile >= ntiles) return;
+  const uint32_t y = tile % nslice, r = tile / nslice;
+  const uint32_t x = r % g.axes, z = r / g.axes;
+  const uint32_t col = y * 256u + lane * 4u;
+  const bool active = col < g.len;
+  const uint32_t lo = active ? lane * 4u : 0u;  // inactive lanes load (and never store) dword 0
+  uint32_t w[K];
+  if constexpr (DBG == 2) {
+#pragma unroll
+    for (int i = 0; i < K; i++) w[i] = (col * 2654435761u) ^ (uint32_t)i;
+  } else {
+    const auto rin = rsrc(g.in + (uint64_t)z * g.in_sq + (uint64_t)x * g.in_axis + (uint64_t)y * 256u);
+    const uint32_t in_shard = (uint32_t)g.in_shard;
+#pragma unroll
+    for (int i = 0; i < K; i++) w[i] = __builtin_amdgcn_raw_buffer_load_b32(rin, lo, (uint32_t)i * in_shard, 0);
+    if (g.dcopy && active) {
+      const auto rdc = rsrc(g.dcopy + (uint64_t)z * g.dc_sq + (uint64_t)x * g.dc_axis + (uint64_t)y * 256u);
+      const uint32_t dc_shard = (uint32_t)g.dc_shard;
+#pragma unroll
+      for (int i = 0; i < K; i++) __builtin_amdgcn_raw_buffer_store_b32(w[i], rdc, lo, (uint32_t)i * dc_shard, 0);
+    }
+  }
+  if constexpr (DBG != 1) transform<K>(w);
+  if constexpr (DBG == 2) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < K; i++) acc ^= w[i];
+    if (acc == (uint32_t)g.in_sq + 0x9E3779B9u) g.out[col] = (uint8_t)acc;  // keeps the transform alive
+  } else if (active) {
+    const auto rout = rsrc(g.out + (uint64_t)z * g.out_sq + (uint64_t)x * g.out_axis + (uint64_t)y * 256u);
+    const uint32_t out_shard = (uint32_t)g.out_shard;
+#pragma unroll
+    for (int i = 0; i < K; i++) __builtin_amdgcn_raw_buffer_store_b32(w[i], rout, lo, (uint32_t)i * out_shard, 0);
+  }
+}
+
+template <int LOGK>
+hipError_t launch(const RsGeom& g, hipStream_t s, int dbg) {
+  const uint32_t nslice = (g.len + 255) / 256;
+  const uint64_t nt = (uint64_t)g.axes * nslice * g.nsq;
+  if (nt > 0xFFFFFFFFull) return hipErrorInvalidValue;
+  const uint32_t ntiles = (uint32_t)nt;
+  const dim3 grid((ntiles + 3) / 4);
+  if (dbg == 1) hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 1>), grid, dim3(256), 0, s, g, nslice, ntiles);
+  else if (dbg == 2) hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 2>), grid, dim3(256), 0, s, g, nslice, ntiles);
+  else hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 0>), grid, dim3(256), 0, s, g, nslice, ntiles);
+  return hipGetLastError();
+}
+
+}  // namespace ax
+
+// Byte offsets must fit the 32-bit buffer offsets: (n - 1) * shard stride + len < 2 GiB.
+hipError_t launch_rs_encode_axis(const RsGeom& g, hipStream_t s) {
+  static const int dbg = [] {
+    const char* e = getenv("CEL_RS_DEBUG");
+    return e ? atoi(e) : 0;
+  }();
+  const uint64_t span = (uint64_t)g.n * (g.in_shard > g.out_shard ? g.in_shard : g.out_shard) + g.len;
+  if (span >= 0x7fffffffull || (g.dcopy && (uint64_t)g.n * g.dc_shard + g.len >= 0x7fffffffull))
+    return hipErrorInvalidValue;
+  switch (g.n) {
+    case 1: return ax::launch<0>(g, s, dbg);
+    case 2: return ax::launch<1>(g, s, dbg);
+    case 4: return ax::launch<2>(g, s, dbg);
+    case 8: return ax::launch<3>(g, s, dbg);
+    case 16: return ax::launch<4>(g, s, dbg);
+    case 32: return ax::launch<5>(g, s, dbg);
+    case 64: return ax::launch<6>(g, s, dbg);
+    case 128: return ax::launch<7>(g, s, dbg);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace cel

@@ -680,20 +680,29 @@ static void launch_gf8(const RsGeom& g, const DeviceTables& t, hipStream_t s) {
 // no LDS exchange); v_perm tables for n >= 32, where the bit-sliced kernel needs the
 // whole 256 KiB granule set of a workgroup in registers (256 VGPRs, one workgroup per
 // CU) and its load/compute/store phases stop overlapping (profiles/r1_rs_impl_ab.txt).
-// CEL_RS_IMPL=perm|bitslice forces one implementation for every n.
+// CEL_RS_IMPL=perm|bitslice|axis forces one implementation for every n.
 static int gf8_impl_override() {
   static const int v = [] {
     const char* e = getenv("CEL_RS_IMPL");
     if (!e) return 0;
     if (std::string(e) == "perm") return 1;
     if (std::string(e) == "bitslice") return 2;
+    if (std::string(e) == "axis") return 3;
     return 0;
   }();
   return v;
 }
 static bool use_perm_gf8(uint32_t n) {
   const int o = gf8_impl_override();
-  if (o) return o == 1;
+  if (o) return o != 2;
+  return n >= 32;
+}
+// Wave-per-axis kernel (rs_axis.hip) for n >= 32: compile-time twiddles, no LDS.
+// k = 128, 32 squares (profiles/r1_axis_ab.txt): 15.2 us/square against 18.1 for
+// k_rs_encode_gf8 (CEL_RS_IMPL=perm).
+static bool use_axis_gf8(uint32_t n) {
+  const int o = gf8_impl_override();
+  if (o) return o == 3;
   return n >= 32;
 }
 
@@ -701,6 +710,7 @@ hipError_t launch_rs_encode(const RsGeom& g, const DeviceTables& t, hipStream_t 
   if (g.axes == 0 || g.nsq == 0) return hipSuccess;
   if (g.blk_log && !((g.n == 256 || g.n == 512) && g.len % 512 == 0)) return hipErrorInvalidValue;
   if (2 * g.n <= 256 && !use_perm_gf8(g.n) && g.len % 32 == 0) return launch_rs_encode_bitslice(g, s);
+  if (2 * g.n <= 256 && use_axis_gf8(g.n)) return launch_rs_encode_axis(g, s);
   if (2 * g.n <= 256) {
     switch (g.n) {
       case 1: launch_gf8<0>(g, t, s); break;
