@@ -79,14 +79,16 @@ struct Mul {
       t1l = vconst<t.t1l>();
     }
   }
-  // x ^= c * y on 4 bytes
-  __device__ __forceinline__ void muladd(uint32_t& x, uint32_t y) const {
+  // x ^= c * y on 4 bytes; m7 = 0x07070707, m3 = 0x03030303 held in SGPRs (a VOP2
+  // with an SGPR operand is 4 bytes against 8 with a literal: the unrolled transform
+  // is ~60 KiB of code, at the size of the instruction cache)
+  __device__ __forceinline__ void muladd(uint32_t& x, uint32_t y, uint32_t m7, uint32_t m3) const {
     if constexpr (kOne) {
       x ^= y;
     } else if constexpr (!kZero) {
-      const uint32_t s0 = y & 0x07070707u;
-      const uint32_t s1 = (y >> 3) & 0x07070707u;
-      const uint32_t s2 = (y >> 6) & 0x03030303u;
+      const uint32_t s0 = y & m7;
+      const uint32_t s1 = (y >> 3) & m7;
+      const uint32_t s2 = (y >> 6) & m3;
       const uint32_t p0 = __builtin_amdgcn_perm(t0h, t0l, s0);
       const uint32_t p1 = __builtin_amdgcn_perm(t1h, t1l, s1);
       const uint32_t p2 = __builtin_amdgcn_perm(0u, t2, s2);
@@ -101,10 +103,23 @@ __device__ __forceinline__ void pin(uint32_t& a, uint32_t& b) { asm volatile("" 
 
 // Leopard IFFT over the data coset (offset K) then FFT over the parity coset (offset 0),
 // radix 2, all K shards in w[]. Skew index: IFFT K-1 + base + D, FFT base + D - 1.
+// The last IFFT layer and the first FFT layer act on the same pairs (a, a + K/2):
+//   y ^= x; x ^= c1*y;  then  x ^= c2*y; y ^= x   ==   y ^= x; x ^= (c1 + c2)*y; y ^= x
+// so they run as one layer with one multiply by c1 + c2 (K/2 of the K log K
+// butterflies lose a multiply).
+constexpr uint32_t merged_lm(uint32_t s1, uint32_t s2) {
+  const uint32_t c = (s1 == 255u ? 0u : (uint32_t)kGf8.exp[s1]) ^ (s2 == 255u ? 0u : (uint32_t)kGf8.exp[s2]);
+  return c == 0u ? 255u : (uint32_t)kGf8.log[c];
+}
+
 template <int K>
 __device__ __forceinline__ void transform(uint32_t (&w)[K]) {
   constexpr int LOGK = __builtin_ctz(K);
-  sfor<LOGK>([&](auto lg) {
+  const uint32_t m7 = sconst<0x07070707u>(), m3 = sconst<0x03030303u>();
+  if constexpr (K == 1) {
+    return;
+  } else {
+  sfor<LOGK - 1>([&](auto lg) {
     constexpr int D = 1 << decltype(lg)::value;
     sfor<K / (2 * D)>([&](auto bi) {
       constexpr int base = decltype(bi)::value * 2 * D;
@@ -113,27 +128,41 @@ __device__ __forceinline__ void transform(uint32_t (&w)[K]) {
         constexpr int a = base + decltype(j)::value;
         pin(w[a], w[a + D]);
         w[a + D] ^= w[a];
-        m.muladd(w[a], w[a + D]);
+        m.muladd(w[a], w[a + D], m7, m3);
         pin(w[a], w[a + D]);
         __builtin_amdgcn_sched_barrier(0);
       });
     });
   });
-  sfor<LOGK>([&](auto t) {
-    constexpr int D = K >> (decltype(t)::value + 1);
+  {
+    constexpr int D = K / 2;
+    const Mul<merged_lm(kGf8.skew[K - 1 + D], kGf8.skew[D - 1])> m;
+    sfor<D>([&](auto j) {
+      constexpr int a = decltype(j)::value;
+      pin(w[a], w[a + D]);
+      w[a + D] ^= w[a];
+      m.muladd(w[a], w[a + D], m7, m3);
+      w[a + D] ^= w[a];
+      pin(w[a], w[a + D]);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  }
+  sfor<LOGK - 1>([&](auto t) {
+    constexpr int D = K >> (decltype(t)::value + 2);
     sfor<K / (2 * D)>([&](auto bi) {
       constexpr int base = decltype(bi)::value * 2 * D;
       const Mul<kGf8.skew[base + D - 1]> m;
       sfor<D>([&](auto j) {
         constexpr int a = base + decltype(j)::value;
         pin(w[a], w[a + D]);
-        m.muladd(w[a], w[a + D]);
+        m.muladd(w[a], w[a + D], m7, m3);
         w[a + D] ^= w[a];
         pin(w[a], w[a + D]);
         __builtin_amdgcn_sched_barrier(0);
       });
     });
   });
+  }
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
@@ -196,6 +225,7 @@ hipError_t launch(const RsGeom& g, hipStream_t s, int dbg) {
   return hipGetLastError();
 }
 
+
 }  // namespace ax
 
 // Byte offsets must fit the 32-bit buffer offsets: (n - 1) * shard stride + len < 2 GiB.
@@ -221,3 +251,4 @@ hipError_t launch_rs_encode_axis(const RsGeom& g, hipStream_t s) {
 }
 
 }  // namespace cel
+

@@ -115,3 +115,25 @@ def test_gf16_square_k512(ctx, oracle):
     assert hashlib.sha256(dev.cells.tobytes()).digest() == hashlib.sha256(eds.tobytes()).digest()
     assert np.array_equal(dev._row_roots, rr) and np.array_equal(dev._col_roots, cr)
     assert dev._dah == dah
+
+
+@pytest.mark.parametrize("k,n", [(32, 3), (64, 9), (128, 5), (128, 17)])
+def test_batch_extension_uneven(ctx, oracle, k, n):
+    """Batches of the wave-per-axis kernel sizes (k = 32..128) with odd square counts
+    (uneven pipeline chunks, partial last workgroup): EDS bytes, roots and DAH against
+    the oracle for every square."""
+    import ctypes
+    from celestia_eds import _lib
+    odss = np.stack([random_ods(k, 900 + 7 * i + k) for i in range(n)])
+    rr = np.zeros((n, 2 * k, 90), np.uint8)
+    cr = np.zeros_like(rr)
+    dah = np.zeros((n, 32), np.uint8)
+    eds = np.zeros((n, 2 * k, 2 * k, 512), np.uint8)
+    st = np.zeros(n, np.int32)
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    ctx.check(ctx.lib.cel_extend_batch(ctx.handle, P(odss), n, k, 512, P(eds), P(rr), P(cr), P(dah), P(st),
+                                       _lib.FLAG_ORDER_CHECK))
+    for i in range(n):
+        e, r, c, d = oracle.extend_and_commit(odss[i])
+        assert np.array_equal(eds[i], e), f"square {i}: EDS differs"
+        assert np.array_equal(rr[i], r) and np.array_equal(cr[i], c) and dah[i].tobytes() == d
