@@ -117,11 +117,11 @@ def test_gf16_square_k512(ctx, oracle):
     assert dev._dah == dah
 
 
-@pytest.mark.parametrize("k,n", [(32, 3), (64, 9), (128, 5), (128, 17)])
+@pytest.mark.parametrize("k,n", [(32, 3), (64, 9), (64, 40), (128, 5), (128, 17)])
 def test_batch_extension_uneven(ctx, oracle, k, n):
-    """Batches of the wave-per-axis kernel sizes (k = 32..128) with odd square counts
-    (uneven pipeline chunks, partial last workgroup): EDS bytes, roots and DAH against
-    the oracle for every square."""
+    """Batches of the wave-per-axis kernel sizes (k = 32..128) with odd square counts:
+    (64, 40) and (128, 17) run the chunked row/column pipeline of launch_extend with a
+    short last chunk; EDS bytes, roots and DAH against the oracle for every square."""
     import ctypes
     from celestia_eds import _lib
     odss = np.stack([random_ods(k, 900 + 7 * i + k) for i in range(n)])
