@@ -191,13 +191,18 @@ __global__ CEL_LEAF_BOUNDS void k_leaf(const uint8_t* __restrict__ eds, uint32_t
   const uint64_t sq_eds = (uint64_t)W * W * kShare;
   const uint32_t* sh = reinterpret_cast<const uint32_t*>(eds + blockIdx.y * sq_eds + (uint64_t)cell * kShare);
   const bool q0 = (r < k) && (c < k);
+  {
+    uint32_t nd[kNodeWords];
+    make_leaf_node(sh, q0, nd);
+    store_node(leaves + ((uint64_t)blockIdx.y * W * W + cell) * kNodeWords, nd);
+  }
+  // The push-order check runs after the hash: done first, its share prefixes stay live
+  // across the nine compressions (103 VGPRs, 4 waves/SIMD, against 52 and 8).
+  __builtin_amdgcn_sched_barrier(0);
   if (ORDER && q0) {
     if (c > 0 && ns_less(sh, sh - kShare / 4)) atomicMin(bad_axis + blockIdx.y, (int32_t)r);
     if (r > 0 && ns_less(sh, sh - (uint64_t)W * kShare / 4)) atomicMin(bad_axis + blockIdx.y, (int32_t)(W + c));
   }
-  uint32_t nd[kNodeWords];
-  make_leaf_node(sh, q0, nd);
-  store_node(leaves + ((uint64_t)blockIdx.y * W * W + cell) * kNodeWords, nd);
 }
 
 // ---------------------------------------------------------------- inner nodes
@@ -249,9 +254,12 @@ __device__ __forceinline__ void rfc_leaf90(const uint32_t (&R)[kNodeWords], uint
 // One tree level for all trees. With LEAFD != nullptr this is the root level: each lane
 // also hashes its root as an RFC-6962 leaf of the DAH tree (2 compressions) so the
 // per-square DAH kernel starts from leaf digests.
+// At the root level (leafd != nullptr) the lane also writes its root, packed to 90
+// bytes, straight into the caller's row_out / col_out ([nsq][W][90]).
 template <bool FROM_LEAVES>
 __global__ CEL_LEVEL_BOUNDS void k_level(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint32_t W,
-                                               uint32_t nin, uint32_t trees, uint32_t* __restrict__ leafd) {
+                                               uint32_t nin, uint32_t trees, uint32_t* __restrict__ leafd,
+                                               uint8_t* __restrict__ row_out, uint8_t* __restrict__ col_out) {
   const uint32_t nout = nin / 2;
   const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
   if (idx >= trees * nout) return;
@@ -273,6 +281,13 @@ __global__ CEL_LEVEL_BOUNDS void k_level(const uint32_t* __restrict__ in, uint32
   const uint64_t oi = (uint64_t)blockIdx.y * trees * nout + idx;
   store_node(out + oi * kNodeWords, o);
   if (leafd) {
+    if (row_out) {  // 90-byte record at a 2-byte aligned address: 45 halfword stores
+      uint8_t* r = (t < W ? row_out + ((uint64_t)blockIdx.y * W + t) * kNode
+                          : col_out + ((uint64_t)blockIdx.y * W + (t - W)) * kNode);
+      uint16_t* r16 = reinterpret_cast<uint16_t*>(r);
+#pragma unroll
+      for (int i = 0; i < 45; i++) r16[i] = (uint16_t)(o[i / 2] >> (16 * (i & 1)));
+    }
     uint32_t st[8];
     rfc_leaf90(o, st);
     uint4* d = reinterpret_cast<uint4*>(leafd + oi * 8);
@@ -451,15 +466,18 @@ hipError_t launch_commit(const uint8_t* eds, uint32_t k, uint32_t nsq, uint8_t* 
     uint32_t* out = (nout == 1) ? roots : dst;
     uint32_t* ld = (nout == 1) ? leafd : nullptr;
     dim3 g((trees * nout + 255) / 256, nsq);
-    if (first) hipLaunchKernelGGL(k_level<true>, g, dim3(256), 0, s, src, out, W, nin, trees, ld);
-    else hipLaunchKernelGGL(k_level<false>, g, dim3(256), 0, s, src, out, W, nin, trees, ld);
+    uint8_t* ro = (nout == 1) ? row_roots : nullptr;
+    uint8_t* co = (nout == 1) ? col_roots : nullptr;
+    if (first) hipLaunchKernelGGL(k_level<true>, g, dim3(256), 0, s, src, out, W, nin, trees, ld, ro, co);
+    else hipLaunchKernelGGL(k_level<false>, g, dim3(256), 0, s, src, out, W, nin, trees, ld, ro, co);
     first = false;
     src = out;
     dst = (dst == ping) ? pong : ping;
     nin = nout;
   }
   const size_t lds = (size_t)trees * 8 * 4;
-  hipLaunchKernelGGL(k_merkle, dim3(nsq), dim3(256), lds, s, roots, leafd, trees, dah, row_roots, col_roots, bad, status);
+  // roots already packed into row_roots / col_roots by the root level
+  hipLaunchKernelGGL(k_merkle, dim3(nsq), dim3(256), lds, s, roots, leafd, trees, dah, nullptr, nullptr, bad, status);
   return hipGetLastError();
 }
 
@@ -553,7 +571,7 @@ static void reduce_grid(const uint32_t* in, uint32_t nin, uint32_t trees, uint32
     nout = nin / 2;
     out = (nout == 1) ? roots : dst;
     hipLaunchKernelGGL(k_level<false>, dim3((trees * nout + 255) / 256, 1), dim3(256), 0, s, src, out, 0u, nin, trees,
-                       nullptr);
+                       nullptr, nullptr, nullptr);
     src = out;
     dst = (dst == ping) ? pong : ping;
     nin = nout;
@@ -820,7 +838,7 @@ hipError_t launch_axes_roots(const uint8_t* cells, uint32_t k, const int32_t* ax
     const uint32_t nout = nin / 2;
     uint32_t* out = (nout == 1) ? roots : dst;
     hipLaunchKernelGGL(k_level<false>, dim3((naxes * nout + 255) / 256, 1), dim3(256), 0, s, src, out, W, nin, naxes,
-                       nullptr);
+                       nullptr, nullptr, nullptr);
     src = out;
     dst = (dst == ping) ? pong : ping;
     nin = nout;

@@ -57,7 +57,7 @@ for cs in a.chunks:
     e1.record(sb.hip_stream)
     e1.synchronize()
     us = e0.elapsed_time(e1) / a.reps * 1e3 / B
-    print(f"{os.environ.get('CEL_RS_IMPL', 'default'):9s} fused={os.environ.get('CEL_RS_FUSED', '1')} dbg={os.environ.get('CEL_RS_DEBUG', '0')} streams={a.streams} k={k} chunk={cs:3d}: {us:6.2f} us/square "
+    print(f"{os.environ.get('CEL_RS_IMPL', 'default'):9s} dbg={os.environ.get('CEL_RS_DEBUG', '0')} streams={a.streams} k={k} chunk={cs:3d}: {us:6.2f} us/square "
           f"= {2048 * k * k / us / 1e3:7.1f} GB/s algorithmic ({2048 * k * k / us / 1e3 / 8000 * 100:4.1f} %)")
 
 if os.environ.get("CEL_COPY_REF"):
