@@ -28,8 +28,29 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table)
-# integer VALU issue peak: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T lane-ops/s
-VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9
+# SHA-256 ceiling for the NMT phase: the compression's instruction mix (per 16 rounds with
+# the message schedule: 160 v_alignbit + 64 v_add3 at 4 cycles per wave64 instruction,
+# 96 v_bitop3 at 2.5, 64 VOP2 at 2; the first 16 rounds without schedule) priced at the
+# measured per-op rates of profiles/r1_microbench_valu.txt is ~4.5k cycles per compression
+# per wave: 1024 SIMDs x 2.4 GHz x 64 / 4528 = 34.7 G compressions/s.
+SHA_MIX_CEILING = 1024 * 2.4e9 * 64 / 4528
+# Measured HBM traffic of the RS extension (rocprofv3 FETCH_SIZE/WRITE_SIZE passes).
+TRAFFIC_PROFILE = os.path.join(ROOT, "profiles", "r1_rs_traffic.json")
+
+
+def _rs_traffic(k, batch):
+    """HBM bytes per RS launch pair from the committed PMC profile, scaled to `batch`
+    squares (per-square traffic is batch-independent at these sizes), or None."""
+    try:
+        with open(TRAFFIC_PROFILE) as f:
+            p = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if p.get("k") != k:
+        return None
+    return {"bytes": p["bytes_per_square"] * batch, "per_square": p["bytes_per_square"],
+            "vs_algorithmic": p["bytes_per_square"] / p["algorithmic_bytes_per_square"],
+            "source": "profiles/r1_rs_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, KiB)"}
 
 
 def parse():
@@ -330,21 +351,23 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "rs_extend (k_rs_encode rows + cols)",
+            "kernel": ("rs_extend (k_rs_axis_gf8 rows + cols launches)" if 32 <= k <= 128
+                       else "rs_extend (rows + cols launches)"),
             "achieved": rs_gbs,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": rs_gbs / HBM_PEAK_GBS,
-            "traffic": None,
+            "traffic": _rs_traffic(k, B),
             "avg_launch_us": t_ext * 1e6,
         },
         "roofline_nmt": {
             "bound": "valu",
-            "kernel": "nmt_commit (k_leaf + k_level + k_top + k_merkle)",
+            "kernel": "nmt_commit (k_leaf + k_level x log2(2k) + k_merkle)",
             "achieved": nmt_rate / 1e9,
             "unit": "G SHA-256 compressions/s",
-            "peak": VALU_LANE_OPS / 1500 / 1e9,
-            "frac": nmt_rate * 1500 / VALU_LANE_OPS,
+            "peak": SHA_MIX_CEILING / 1e9,
+            "peak_basis": "SHA-256 instruction mix at measured per-op VALU rates (profiles/r1_microbench_valu.txt)",
+            "frac": nmt_rate / SHA_MIX_CEILING,
             "avg_launch_us": t_com * 1e6,
         },
     }

@@ -9,7 +9,8 @@ template <int OP>
 __global__ __launch_bounds__(256) void k_rate(uint32_t* out, uint32_t seed, int iters) {
   uint32_t a[N_ACC];
   float f[N_ACC];
-  for (int i = 0; i < N_ACC; i++) { a[i] = seed * (threadIdx.x + 1) + i; f[i] = (float)a[i]; }
+  uint64_t b[N_ACC];
+  for (int i = 0; i < N_ACC; i++) { a[i] = seed * (threadIdx.x + 1) + i; f[i] = (float)a[i]; b[i] = ((uint64_t)a[i] << 32) | a[i]; }
   for (int it = 0; it < iters; it++) {
 #pragma unroll
     for (int r = 0; r < 16; r++)
@@ -21,10 +22,14 @@ __global__ __launch_bounds__(256) void k_rate(uint32_t* out, uint32_t seed, int 
         if (OP == 3) a[i] = a[i] + a[(i + 1) % N_ACC] + a[(i + 2) % N_ACC];  // v_add3
         if (OP == 4) f[i] = __builtin_fmaf(f[i], 1.0001f, f[(i + 1) % N_ACC]);
         if (OP == 5) a[i] = __builtin_amdgcn_perm(a[i], a[(i + 1) % N_ACC], 0x05040100u + r);
+        if (OP == 6) asm volatile("v_lshrrev_b64 %0, 7, %1" : "=v"(b[i]) : "v"(b[(i + 1) % N_ACC]));
+        if (OP == 7) a[i] = (a[(i + 1) % N_ACC] << 7) | a[i];  // v_lshl_or_b32
+        if (OP == 8) a[i] = __builtin_amdgcn_alignbyte(a[i], a[(i + 1) % N_ACC], 3);
+        if (OP == 9) a[i] = a[i] + a[(i + 1) % N_ACC];  // v_add_u32 alone
       }
   }
   uint32_t s = 0;
-  for (int i = 0; i < N_ACC; i++) s ^= a[i] ^ __float_as_uint(f[i]);
+  for (int i = 0; i < N_ACC; i++) s ^= a[i] ^ __float_as_uint(f[i]) ^ (uint32_t)b[i];
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
@@ -80,8 +85,8 @@ int main() {
   uint32_t* out;
   hipMalloc(&out, 256 * 8 * 512 * 4 * 8);
   const int iters = 200;
-  const char* names[] = {"xor+add (2 ops)", "bitop3", "alignbit", "add3", "fma_f32", "perm"};
-  for (int op = 0; op < 6; op++) {
+  const char* names[] = {"xor+add (2 ops)", "bitop3", "alignbit", "add3", "fma_f32", "perm", "lshrrev_b64", "lshl_or", "alignbyte", "add_u32"};
+  for (int op = 0; op < 10; op++) {
     for (int wpc : {4, 8, 16}) {  // waves per CU
       dim3 grid(256 * wpc / 4), block(256);
       float ms = 0;
@@ -92,6 +97,10 @@ int main() {
         case 3: ms = time_kernel(k_rate<3>, grid, block, out, iters); break;
         case 4: ms = time_kernel(k_rate<4>, grid, block, out, iters); break;
         case 5: ms = time_kernel(k_rate<5>, grid, block, out, iters); break;
+        case 6: ms = time_kernel(k_rate<6>, grid, block, out, iters); break;
+        case 7: ms = time_kernel(k_rate<7>, grid, block, out, iters); break;
+        case 8: ms = time_kernel(k_rate<8>, grid, block, out, iters); break;
+        case 9: ms = time_kernel(k_rate<9>, grid, block, out, iters); break;
       }
       const double ops = (double)grid.x * 256 * iters * 16 * N_ACC * (op == 0 ? 2 : 1);
       printf("%-16s waves/CU=%2d  %8.3f ms  %7.2f T lane-ops/s\n", names[op], wpc, ms, ops / (ms * 1e-3) / 1e12);
