@@ -27,7 +27,7 @@ EXPORTS = [
     "cel_dev_extend_only", "cel_dev_commit_only", "cel_codec_encode", "cel_codec_decode",
     "cel_codec_max_chunks", "cel_codec_name", "cel_codec_validate_chunk_size", "cel_axis_root",
     "cel_nmt_root", "cel_dah_hash", "cel_repair", "cel_dev_shard_workspace_size", "cel_dev_shard_rows",
-    "cel_dev_shard_cols", "cel_dev_shard_finish",
+    "cel_dev_shard_cols", "cel_dev_shard_finish", "cel_square_construct", "cel_square_last_error",
 ]
 
 _lib = None
@@ -76,6 +76,8 @@ def load():
             "cel_dev_shard_rows": (i32, [P, P, u32, u32, P, P]),
             "cel_dev_shard_cols": (i32, [P, P, u32, u32, u32, P, P, P, P, P, u32]),
             "cel_dev_shard_finish": (i32, [P, P, P, u32, u32, P, P, P, P, P, P, u32]),
+            "cel_square_construct": (i32, [P, P, u32, u32, u32, u32, P, u32, P, P]),
+            "cel_square_last_error": (ctypes.c_char_p, []),
         }
         for name, (res, args) in sigs.items():
             fn = getattr(l, name)

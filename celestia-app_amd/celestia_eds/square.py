@@ -1,0 +1,69 @@
+"""go-square v1.1.0 data-square construction, mirrored over the
+C ABI's cel_square_construct (host code in csrc/square.cpp, no device needed).
+
+  Construct(txs, max_square_size, subtree_root_threshold)
+      square.Construct as called by app/extend_block.go:16-25 and
+      app/process_proposal.go:121-130: the exact ordered tx list -> the k*k shares
+      handed to da.ExtendShares; raises CelError if a tx does not fit or a normal tx
+      follows a blob tx (go-square's error strings).
+  Build(txs, max_square_size, subtree_root_threshold)
+      square.Build as called by app/prepare_proposal.go:48-61: greedy, drops what does
+      not fit; returns (shares, kept txs with normal txs before blob txs).
+
+The defaults are appconsts SquareSizeUpperBound = 128 and SubtreeRootThreshold = 64
+(pkg/appconsts/v1,v2/app_consts.go).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+
+SQUARE_SIZE_UPPER_BOUND = 128
+SUBTREE_ROOT_THRESHOLD = 64
+
+
+def _call(txs, max_square_size, subtree_root_threshold, greedy):
+    l = _lib.load()
+    txs = [bytes(t) for t in txs]
+    lens = (ctypes.c_uint32 * max(len(txs), 1))(*[len(t) for t in txs])
+    blob = b"".join(txs)
+    buf = ctypes.create_string_buffer(blob, max(len(blob), 1))
+    k = ctypes.c_uint32()
+    included = (ctypes.c_uint8 * max(len(txs), 1))()
+
+    def run(out, cap):
+        return l.cel_square_construct(buf, lens, len(txs), max_square_size, subtree_root_threshold, greedy,
+                                      out, cap, ctypes.byref(k), included)
+
+    st = run(None, 0)
+    if st != _lib.OK:
+        raise _lib.CelError(st, l.cel_square_last_error().decode())
+    n = k.value * k.value
+    out = np.zeros((n, _lib.SHARE_SIZE), np.uint8)
+    st = run(out.ctypes.data_as(ctypes.c_void_p), n)
+    if st != _lib.OK:
+        raise _lib.CelError(st, l.cel_square_last_error().decode())
+    return out, [bool(included[i]) for i in range(len(txs))]
+
+
+def Construct(txs, max_square_size=SQUARE_SIZE_UPPER_BOUND, subtree_root_threshold=SUBTREE_ROOT_THRESHOLD):
+    """-> uint8 array [k*k][512]: the ODS shares (shares.ToBytes of the square)."""
+    return _call(txs, max_square_size, subtree_root_threshold, 0)[0]
+
+
+def Build(txs, max_square_size=SQUARE_SIZE_UPPER_BOUND, subtree_root_threshold=SUBTREE_ROOT_THRESHOLD):
+    """-> (shares [k*k][512], kept txs: normal txs first, then blob txs)."""
+    out, kept = _call(txs, max_square_size, subtree_root_threshold, 1)
+    normal, blob = [], []
+    for t, keep in zip(txs, kept):
+        if keep:
+            (blob if is_blob_tx(t) else normal).append(bytes(t))
+    return out, normal + blob
+
+
+def is_blob_tx(tx):
+    """blob.UnmarshalBlobTx's verdict, through a one-tx greedy build (a blob tx lands in
+    the PFB namespace of the square)."""
+    out, kept = _call([tx], SQUARE_SIZE_UPPER_BOUND, SUBTREE_ROOT_THRESHOLD, 1)
+    return bool(kept[0]) and bytes(out[0][:29]) == bytes(28) + b"\x04"

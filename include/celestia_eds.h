@@ -174,6 +174,27 @@ cel_status cel_repair(cel_ctx* ctx, uint8_t* eds, uint8_t* present, uint32_t k,
                       uint32_t share_size, const uint8_t* row_roots, const uint8_t* col_roots,
                       int32_t* bad_axis, int32_t* bad_index);
 
+/* ---------------------------------------------------- data-square construction
+ * go-square v1.1.0 (host code, no device needed):
+ *   greedy = 0: square.Construct (app/extend_block.go:16-25, app/process_proposal.go:121-130):
+ *               normal txs must precede blob txs; a tx that does not fit is an error
+ *               (CEL_ETOOBIG "not enough space to append tx at index i",
+ *               CEL_EINVAL "normal transaction at index i can not be appended after blob tx");
+ *   greedy = 1: square.Build (app/prepare_proposal.go:48-61): txs that do not fit are
+ *               skipped; included[i] (nullable, ntx bytes) reports which were kept
+ *               (the square orders kept normal txs before kept blob txs).
+ * txs: the ntx transactions concatenated, tx_lens[ntx] their lengths.
+ * max_square_size / subtree_root_threshold: appconsts SquareSizeUpperBound (128) and
+ * SubtreeRootThreshold (64) (pkg/appconsts/v1,v2/app_consts.go).
+ * Writes k*k shares (the ODS handed to cel_extend_shares) to shares_out (capacity
+ * cap_shares shares; shares_out == NULL only reports *k_out). */
+cel_status cel_square_construct(const uint8_t* txs, const uint32_t* tx_lens, uint32_t ntx,
+                                uint32_t max_square_size, uint32_t subtree_root_threshold,
+                                uint32_t greedy, uint8_t* shares_out, uint32_t cap_shares,
+                                uint32_t* k_out, uint8_t* included);
+/* Message of the last cel_square_construct failure on this thread. */
+const char* cel_square_last_error(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -139,6 +139,8 @@ def compact_shares(ns: bytes, units) -> list:
 
 def compact_share_count(units) -> int:
     total = sum(len(uvarint(len(u))) + len(u) for u in units)
+    if total == 0:  # shares.CompactShareCounter.Size() of an empty sequence
+        return 0
     if total <= SHARE - NS - 1 - 4 - 4:
         return 1
     rest = total - (SHARE - NS - 1 - 4 - 4)

@@ -2,6 +2,8 @@
 container, where /root/reference exists; the GPU box only reads the outputs).
 
 Fixtures:
+  block408_txs.bin.gz  the 408 block's transactions as in the reference fixture
+                       (data, not code): records of u32 little-endian length || tx bytes
   block408_ods.bin.gz  the k=32 ODS of mainnet block 408, built from
                        /root/reference/x/blob/test/testdata/block_response.json by the
                        go-square layout restatement in oracle/square_layout.py
@@ -38,13 +40,18 @@ def model_data(k):
 def main():
     oracle.set_simd(True)
     k, ods, data_hash, height = square_layout.block408_ods(REF_JSON)
+    with open(REF_JSON) as f:
+        txs = [base64.b64decode(t) for t in json.load(f)["block"]["data"]["txs"]]
+    with gzip.open(os.path.join(HERE, "block408_txs.bin.gz"), "wb", compresslevel=9) as f:
+        for t in txs:
+            f.write(len(t).to_bytes(4, "little") + t)
     with gzip.open(os.path.join(HERE, "block408_ods.bin.gz"), "wb", compresslevel=9) as f:
         f.write(ods)
     eds, rr, cr, dah = oracle.extend_and_commit(np.frombuffer(ods, np.uint8).reshape(k, k, 512))
     assert dah == data_hash, "oracle does not reproduce block 408"
     golden = {
         "block408": {
-            "height": height, "k": k,
+            "height": height, "k": k, "ntx": len(txs),
             "data_hash": data_hash.hex(),
             "ods_sha256": hashlib.sha256(ods).hexdigest(),
             "eds_sha256": hashlib.sha256(eds.tobytes()).hexdigest(),

@@ -137,3 +137,22 @@ def test_batch_extension_uneven(ctx, oracle, k, n):
         e, r, c, d = oracle.extend_and_commit(odss[i])
         assert np.array_equal(eds[i], e), f"square {i}: EDS differs"
         assert np.array_equal(rr[i], r) and np.array_equal(cr[i], c) and dah[i].tobytes() == d
+
+
+def test_extend_block_408_from_txs(ctx, golden):
+    """app.ExtendBlock (app/extend_block.go:14-26) end to end through the product:
+    block 408's txs -> square.Construct (cel_square_construct) -> da.ExtendShares ->
+    NewDataAvailabilityHeader on the device == the block header's data_hash."""
+    from celestia_eds import da, square
+    from square_inputs import block408_txs
+    ods = square.Construct(block408_txs())
+    eds = da.ExtendShares(list(ods))
+    assert da.NewDataAvailabilityHeader(eds).Hash().hex() == golden["block408"]["data_hash"]
+
+
+def test_extend_empty_block(ctx, golden):
+    """An empty block's square is one tail-padding share: its DAH is the reference's
+    MinDataAvailabilityHeader hash (data_availability_header_test.go:27-32)."""
+    from celestia_eds import da, square
+    eds = da.ExtendShares(list(square.Construct([])))
+    assert da.NewDataAvailabilityHeader(eds).Hash().hex() == golden["dah_known_answers"]["min"]

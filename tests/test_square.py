@@ -1,0 +1,98 @@
+"""Data-square construction (go-square v1.1.0 square.Construct / square.Build, SURVEY.md
+§8f row 1): the product's cel_square_construct (host C++, csrc/square.cpp) against
+  - mainnet block 408: its txs must give the committed ODS, whose data root is the
+    block's data_hash (golden.json; pinned through the oracle in test_oracle.py);
+  - the oracle restatement (oracle/square_layout.py) on synthetic blocks;
+  - go-square's error behaviour (normal tx after a blob tx, no space) and Build's greedy
+    admission.
+Host logic only: no device needed."""
+import gzip
+import os
+
+import numpy as np
+import pytest
+
+from square_inputs import blob_tx, block408_txs, random_block
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _oracle_square(txs):
+    import square_layout
+    k, shares = square_layout.build_square(txs)
+    return k, np.frombuffer(b"".join(shares), np.uint8).reshape(-1, 512)
+
+
+def test_block408_layout(golden):
+    from celestia_eds import square
+    txs = block408_txs()
+    assert len(txs) == golden["block408"]["ntx"]
+    ods = square.Construct(txs)
+    ref = np.frombuffer(gzip.open(os.path.join(ROOT, "tests", "golden", "block408_ods.bin.gz")).read(), np.uint8)
+    assert ods.shape == (golden["block408"]["k"] ** 2, 512)
+    assert np.array_equal(ods.reshape(-1), ref)
+
+
+@pytest.mark.parametrize("seed,n_normal,n_blob", [(1, 0, 1), (2, 5, 0), (3, 12, 4), (4, 40, 20), (5, 3, 60),
+                                                  (6, 200, 2), (7, 0, 30)])
+def test_matches_oracle_layout(seed, n_normal, n_blob):
+    from celestia_eds import square
+    txs = random_block(seed, n_normal, n_blob)
+    ods = square.Construct(txs)
+    k, ref = _oracle_square(txs)
+    assert ods.shape == ref.shape == (k * k, 512)
+    assert np.array_equal(ods, ref)
+
+
+def test_small_blobs_share_one_namespace_padding():
+    """Many one-share blobs in two namespaces: stable namespace sort, tx order kept
+    inside a namespace."""
+    from celestia_eds import square
+    a, b = bytes(27) + b"\x02", bytes(27) + b"\x01"
+    txs = [blob_tx(b"inner%d" % i, [(a if i % 2 else b, bytes([i]) * 100)]) for i in range(10)]
+    ods = square.Construct(txs)
+    k, ref = _oracle_square(txs)
+    assert np.array_equal(ods, ref)
+    blob_shares = [s for s in ods if bytes(s[1:29]) in (a, b) and s[29] & 1]
+    assert [bytes(s[1:29]) for s in blob_shares] == [b] * 5 + [a] * 5
+    assert [s[34] for s in blob_shares] == [0, 2, 4, 6, 8, 1, 3, 5, 7, 9]
+
+
+def test_empty_block_is_one_tail_padding_share():
+    from celestia_eds import square
+    ods = square.Construct([])
+    assert ods.shape == (1, 512)
+    assert bytes(ods[0][:29]) == b"\xff" * 28 + b"\xfe" and ods[0][29] == 1 and not ods[0][30:].any()
+
+
+def test_construct_errors():
+    from celestia_eds import CelError, _lib, square
+    txs = random_block(9, 2, 1)
+    with pytest.raises(CelError, match="normal transaction at index 2 can not be appended after blob tx") as ei:
+        square.Construct([txs[0], txs[2], txs[1]])  # txs[2] is the blob tx
+    assert ei.value.status == _lib.EINVAL
+    big = [b"\x07" * 400_000] * 30  # ~12M bytes of compact shares > 128^2 shares
+    with pytest.raises(CelError, match=r"not enough space to append tx at index \d+") as ei:
+        square.Construct(big)
+    assert ei.value.status == _lib.ETOOBIG
+
+
+def test_build_is_greedy():
+    from celestia_eds import square
+    big = b"\x07" * 8_000_000  # larger than a 128 x 128 square
+    normal = random_block(11, 3, 0)
+    blobs = random_block(12, 0, 2)
+    txs = [blobs[0], normal[0], big, normal[1], blobs[1], normal[2]]
+    ods, kept = square.Build(txs)
+    assert kept == normal + blobs  # oversized tx dropped; normal txs first
+    assert np.array_equal(ods, square.Construct(kept))
+
+
+def test_worst_case_square_fits_max():
+    """A block filling most of a 128 x 128 square stays within SquareSizeUpperBound."""
+    from celestia_eds import square
+    txs = random_block(13, 0, 40, max_blob=180_000, blobs_per_tx=(1, 1))
+    ods, kept = square.Build(txs)
+    assert ods.shape[0] <= 128 * 128 and len(kept) >= 1
+    k, ref = _oracle_square(kept)
+    assert np.array_equal(ods, ref)
