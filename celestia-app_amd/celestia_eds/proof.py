@@ -1,0 +1,310 @@
+"""pkg/proof mirror: share inclusion proofs to the data root.
+
+Construction (NewShareInclusionProofFromEDS, pkg/proof/proof.go:78-140, and
+CreateShareToRowRootProofs, :147-202) reads the NMT nodes of the rows that hold the
+shares from the device (cel_axis_trees: every node of those row trees, hashed on the
+MI355X) and the row-root proofs from the device-built RFC-6962 tree over
+rowRoots || colRoots (cel_dah_tree); cel_nmt_prove_range / cel_merkle_aunts pick the
+proof nodes (nmt ProveRange, merkle.ProofsFromByteSlices). The reference instead
+rebuilds every row tree on the CPU.
+
+Verification (ShareProof.Validate / VerifyProof, share_proof.go:15-82; RowProof,
+row_proof.go:12-48) mirrors the reference on the host: nmt VerifyInclusion (nmt
+v0.22.0 proof.go [dep]: leaf hashing with the namespace prefix, completeness check,
+computeRoot) and go-square merkle Proof.Verify (RFC-6962). Host-side hashing is the
+reference's own choice for verifiers (a light client verifies on its CPU).
+"""
+import ctypes
+import hashlib
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+
+from . import _lib
+from ._lib import CelError
+
+NS = _lib.NAMESPACE_SIZE
+NODE = _lib.NMT_NODE_SIZE
+PARITY_NS = b"\xff" * NS
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+# --------------------------------------------------------------------- hashing
+def _sha(b):
+    return hashlib.sha256(b).digest()
+
+
+def _nmt_leaf(ns, data):
+    """nmt HashLeaf: ns || ns || SHA256(0x00 || ns || data) (data without the ns prefix)."""
+    return ns + ns + _sha(b"\x00" + ns + data)
+
+
+def _nmt_node(left, right, nsz=NS):
+    """nmt HashNode with IgnoreMaxNamespace (test/util/malicious/hasher.go:186-310 text copy):
+    minNs = L.min; maxNs = L.max if R.min is the max namespace (0xFF * nsz) else
+    max(L.max, R.max). Children must be ordered (L.max <= R.min). nmt is generic in the
+    namespace size: the app uses 29 bytes, nsz follows the verified namespace."""
+    lmin, lmax, rmin, rmax = left[:nsz], left[nsz:2 * nsz], right[:nsz], right[nsz:2 * nsz]
+    if lmax > rmin:
+        raise ValueError("unordered nmt children")
+    mx = lmax if rmin == b"\xff" * nsz else (rmax if rmax > lmax else lmax)
+    return lmin + mx + _sha(b"\x01" + left + right)
+
+
+def _split_point(n):
+    """largest power of two strictly less than n (n >= 2)"""
+    k = 1
+    while k * 2 < n:
+        k *= 2
+    return k
+
+
+def _rfc_leaf(item):
+    return _sha(b"\x00" + item)
+
+
+def _rfc_inner(left, right):
+    return _sha(b"\x01" + left + right)
+
+
+# -------------------------------------------------------------------- types
+@dataclass
+class NMTProof:
+    """proof.NMTProof (proto/celestia/core/v1/proof/proof.proto): nmt range proof."""
+    Start: int
+    End: int
+    Nodes: List[bytes]
+    LeafHash: Optional[bytes] = None
+
+    def VerifyInclusion(self, namespace, leaves, root):
+        """nmt Proof.VerifyInclusion: recompute the root from the leaves (all in `namespace`,
+        given without the namespace prefix) and the proof nodes. Like nmt, no completeness
+        check: the leaves may be a subset of the namespace's leaves (VerifyNamespace is
+        the completeness-checking form)."""
+        start, end = self.Start, self.End
+        nsz = len(namespace)
+        if start < 0 or end <= start or len(leaves) != end - start:
+            return False
+        hashes = [_nmt_leaf(namespace, d) for d in leaves]
+        nodes = list(self.Nodes)
+        state = {"nodes": nodes, "leaves": hashes}
+
+        def pop(key):
+            lst = state[key]
+            if not lst:
+                return None
+            v = lst[0]
+            state[key] = lst[1:]
+            return v
+
+        def compute(s, e):
+            if e - s == 1:
+                return pop("leaves") if start <= s < end else pop("nodes")
+            if e <= start or s >= end:
+                return pop("nodes")
+            k = _split_point(e - s)
+            lh = compute(s, s + k)
+            rh = compute(s + k, e)
+            if rh is None:
+                return lh
+            return _nmt_node(lh, rh, nsz)
+
+        est = max(_split_point(end) * 2 if end > 1 else 1, 1)
+        try:
+            h = compute(0, est)
+            for n in state["nodes"]:
+                h = _nmt_node(h, n, nsz)
+        except ValueError:
+            return False
+        return h == root
+
+
+@dataclass
+class Proof:
+    """merkle.Proof (RFC-6962) of one item among Total."""
+    Total: int
+    Index: int
+    LeafHash: bytes
+    Aunts: List[bytes]
+
+    def _compute(self, index, total, leaf, aunts):
+        if total == 1:
+            return leaf if not aunts else None
+        if not aunts:
+            return None
+        k = _split_point(total)
+        if index < k:
+            lh = self._compute(index, k, leaf, aunts[:-1])
+            return None if lh is None else _rfc_inner(lh, aunts[-1])
+        rh = self._compute(index - k, total - k, leaf, aunts[:-1])
+        return None if rh is None else _rfc_inner(aunts[-1], rh)
+
+    def Verify(self, root, leaf):
+        """go-square merkle Proof.Verify: error (CelError) unless leaf is item Index of root."""
+        if self.Total < 0 or self.Index < 0:
+            raise CelError(_lib.EINVAL, "proof total and index must be non-negative")
+        if _rfc_leaf(leaf) != self.LeafHash:
+            raise CelError(_lib.EINVAL, "invalid leaf hash")
+        if self._compute(self.Index, self.Total, self.LeafHash, list(self.Aunts)) != root:
+            raise CelError(_lib.EINVAL, "invalid root hash")
+
+
+@dataclass
+class RowProof:
+    RowRoots: List[bytes]
+    Proofs: List[Proof]
+    StartRow: int
+    EndRow: int
+
+    def Validate(self, root):
+        if self.EndRow - self.StartRow + 1 != len(self.RowRoots):
+            raise CelError(_lib.EINVAL, f"the number of rows {self.EndRow - self.StartRow + 1} must equal the "
+                                        f"number of row roots {len(self.RowRoots)}")
+        if len(self.Proofs) != len(self.RowRoots):
+            raise CelError(_lib.EINVAL, f"the number of proofs {len(self.Proofs)} must equal the number of row "
+                                        f"roots {len(self.RowRoots)}")
+        if not self.VerifyProof(root):
+            raise CelError(_lib.EINVAL, "row proof failed to verify")
+
+    def VerifyProof(self, root):
+        for p, r in zip(self.Proofs, self.RowRoots):
+            try:
+                p.Verify(root, r)
+            except CelError:
+                return False
+        return True
+
+
+@dataclass
+class ShareProof:
+    Data: List[bytes]
+    ShareProofs: List[NMTProof]
+    NamespaceId: bytes
+    RowProof: RowProof
+    NamespaceVersion: int = 0
+
+    def Validate(self, root):
+        if not self.Data:
+            raise CelError(_lib.EINVAL, "empty share proof")
+        n = sum(p.End - p.Start for p in self.ShareProofs)
+        if len(self.ShareProofs) != len(self.RowProof.RowRoots):
+            raise CelError(_lib.EINVAL, f"the number of share proofs {len(self.ShareProofs)} must equal the "
+                                        f"number of row roots {len(self.RowProof.RowRoots)}")
+        if len(self.Data) != n:
+            raise CelError(_lib.EINVAL, f"the number of shares {len(self.Data)} must equal the number of shares "
+                                        f"in share proofs {n}")
+        for p in self.ShareProofs:
+            if p.Start < 0:
+                raise CelError(_lib.EINVAL, "proof index cannot be negative")
+            if p.End - p.Start <= 0:
+                raise CelError(_lib.EINVAL, "proof total must be positive")
+        self.RowProof.Validate(root)
+        if not self.VerifyProof():
+            raise CelError(_lib.EINVAL, "share proof failed to verify")
+
+    def VerifyProof(self):
+        if self.NamespaceVersion > 255:
+            return False
+        ns = bytes([self.NamespaceVersion]) + bytes(self.NamespaceId)
+        cursor = 0
+        for i, p in enumerate(self.ShareProofs):
+            used = p.End - p.Start
+            if not p.VerifyInclusion(ns, self.Data[cursor:cursor + used], self.RowProof.RowRoots[i]):
+                return False
+            cursor += used
+        return True
+
+
+# ---------------------------------------------------------------- construction
+def axis_trees(eds, axis, first, count, ctx=None):
+    """All nodes of the NMTs of EDS rows (axis 0) or columns (1) [first, first+count):
+    array [count][4k-1][90] (level-major from the leaves), hashed on the device."""
+    ctx = ctx or eds.ctx
+    cells = np.ascontiguousarray(eds.cells)
+    W = cells.shape[0]
+    out = np.zeros((count, 2 * W - 1, NODE), np.uint8)
+    ctx.check(ctx.lib.cel_axis_trees(ctx.handle, _p(cells), W // 2, _lib.SHARE_SIZE, axis, first, count, _p(out)))
+    return out
+
+
+def dah_tree(eds, ctx=None):
+    """RFC-6962 levels over rowRoots || colRoots: array [4w-1][32], root last."""
+    ctx = ctx or eds.ctx
+    rr = np.ascontiguousarray(np.frombuffer(b"".join(eds.RowRoots()), np.uint8))
+    cr = np.ascontiguousarray(np.frombuffer(b"".join(eds.ColRoots()), np.uint8))
+    w = len(eds.RowRoots())
+    out = np.zeros((4 * w - 1, 32), np.uint8)
+    ctx.check(ctx.lib.cel_dah_tree(ctx.handle, _p(rr), _p(cr), w, _p(out)))
+    return out
+
+
+def nmt_prove_range(tree, start, end):
+    """nmt ProveRange(start, end) over one tree of axis_trees(): the proof nodes."""
+    l = _lib.load()
+    tree = np.ascontiguousarray(tree)
+    nleaves = (tree.shape[0] + 1) // 2
+    cnt = ctypes.c_uint32()
+    out = np.zeros((64, NODE), np.uint8)
+    st = l.cel_nmt_prove_range(_p(tree), nleaves, start, end, _p(out), ctypes.byref(cnt))
+    if st != _lib.OK:
+        raise CelError(st, f"invalid proof range [{start}, {end}) over {nleaves} leaves")
+    return [out[i].tobytes() for i in range(cnt.value)]
+
+
+def merkle_aunts(levels, n, index):
+    l = _lib.load()
+    levels = np.ascontiguousarray(levels)
+    cnt = ctypes.c_uint32()
+    out = np.zeros((64, 32), np.uint8)
+    st = l.cel_merkle_aunts(_p(levels), n, index, _p(out), ctypes.byref(cnt))
+    if st != _lib.OK:
+        raise CelError(st, f"invalid merkle index {index} of {n}")
+    return [out[i].tobytes() for i in range(cnt.value)]
+
+
+def CreateShareToRowRootProofs(eds, start_row, end_row, start_leaf, end_leaf):
+    """pkg/proof/proof.go:147-202 on device-built trees: per row, the nmt range proof of
+    the selected shares and the raw shares."""
+    W = eds.Width()
+    trees = axis_trees(eds, 0, start_row, end_row - start_row + 1)
+    share_proofs, raw = [], []
+    roots = eds.RowRoots()
+    for i, r in enumerate(range(start_row, end_row + 1)):
+        if trees[i, -1].tobytes() != roots[r]:
+            raise CelError(_lib.EINVAL, "eds row root is different than tree root")
+        s = start_leaf if i == 0 else 0
+        e = end_leaf if r == end_row else W - 1
+        raw += [eds.GetCell(r, c) for c in range(s, e + 1)]
+        share_proofs.append(NMTProof(Start=s, End=e + 1, Nodes=nmt_prove_range(trees[i], s, e + 1)))
+    return share_proofs, raw
+
+
+def NewShareInclusionProofFromEDS(eds, namespace, share_start, share_end):
+    """pkg/proof/proof.go:78-140: ShareProof of ODS shares [share_start, share_end) (all in
+    `namespace`, 29 bytes) to the data root of `eds`."""
+    k = eds.Width() // 2
+    if not 0 <= share_start < share_end <= k * k:
+        raise CelError(_lib.EINVAL, f"share range [{share_start}, {share_end}) outside the {k}x{k} square")
+    start_row, end_row = share_start // k, (share_end - 1) // k
+    start_leaf, end_leaf = share_start % k, (share_end - 1) % k
+    levels = dah_tree(eds)
+    n = 4 * k
+    roots = eds.RowRoots()
+    proofs = []
+    for r in range(start_row, end_row + 1):
+        proofs.append(Proof(Total=n, Index=r, LeafHash=levels[r].tobytes(), Aunts=merkle_aunts(levels, n, r)))
+    share_proofs, raw = CreateShareToRowRootProofs(eds, start_row, end_row, start_leaf, end_leaf)
+    ns = bytes(namespace)
+    return ShareProof(Data=raw, ShareProofs=share_proofs, NamespaceId=ns[1:], NamespaceVersion=ns[0],
+                      RowProof=RowProof(RowRoots=[roots[r] for r in range(start_row, end_row + 1)], Proofs=proofs,
+                                        StartRow=start_row, EndRow=end_row))
+
+
+def NewShareInclusionProof(ods_shares, namespace, share_start, share_end):
+    """pkg/proof/proof.go:64-76: extend the ODS on the device, then prove."""
+    from . import da
+    return NewShareInclusionProofFromEDS(da.ExtendShares(ods_shares), namespace, share_start, share_end)

@@ -568,6 +568,95 @@ cel_status cel_dah_hash(cel_ctx* ctx, const uint8_t* row_roots, const uint8_t* c
   return CEL_OK;
 }
 
+// ------------------------------------------------------------- exported trees
+//
+// Inner nodes for proofs: pkg/proof/proof.go:151-201 rebuilds
+// each row's NMT on the CPU to call ProveRange; here the device hashes the trees and
+// hands every node back, and the host proof builders (proof.cpp) only pick nodes.
+
+cel_status cel_axis_trees(cel_ctx* ctx, const uint8_t* eds, uint32_t k, uint32_t share_size, uint32_t axis,
+                          uint32_t first, uint32_t count, uint8_t* nodes_out) {
+  if (!ctx) return CEL_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (!eds || !nodes_out || !count) return fail(ctx, CEL_EINVAL, "nil argument");
+  cel_status st = validate_square(ctx, k, share_size);
+  if (st) return st;
+  const uint32_t W = 2 * k;
+  if (axis > 1 || first >= W || count > W - first) return fail(ctx, CEL_EINVAL, "axis range outside the square");
+  DeviceGuard g(ctx->device);
+  hipError_t e = hipSuccess;
+  const size_t cells_b = (size_t)count * W * kShare;
+  const size_t nodes = axes_trees_nodes(k, count);
+  uint8_t* d_c = static_cast<uint8_t*>(scratch(ctx, S_IN, cells_b, &e));
+  uint32_t* d_n = static_cast<uint32_t*>(scratch(ctx, S_WORK, nodes * kNodeWords * 4, &e));
+  int32_t* d_idx = static_cast<int32_t*>(scratch(ctx, S_AUX, (size_t)count * 4, &e));
+  if (!d_c || !d_n || !d_idx) return fail(ctx, CEL_ENOMEM, "device allocation failed");
+  // gather the axes densely on the host: rows are contiguous, columns strided
+  std::vector<uint8_t> cells(cells_b);
+  std::vector<int32_t> idx(count);
+  for (uint32_t a = 0; a < count; a++) {
+    idx[a] = (int32_t)(first + a);
+    for (uint32_t j = 0; j < W; j++) {
+      const size_t cell = axis == 0 ? (size_t)(first + a) * W + j : (size_t)j * W + first + a;
+      std::memcpy(&cells[((size_t)a * W + j) * kShare], eds + cell * kShare, kShare);
+    }
+  }
+  hipStream_t s = ctx->stream;
+  if ((e = hipMemcpyAsync(d_c, cells.data(), cells_b, hipMemcpyHostToDevice, s)) != hipSuccess ||
+      (e = hipMemcpyAsync(d_idx, idx.data(), (size_t)count * 4, hipMemcpyHostToDevice, s)) != hipSuccess)
+    return hip_fail(ctx, e, "H2D");
+  if ((e = launch_axes_trees(d_c, k, d_idx, count, d_n, s)) != hipSuccess) return hip_fail(ctx, e, "axis trees");
+  std::vector<uint32_t> recs(nodes * kNodeWords);
+  if ((e = hipMemcpyAsync(recs.data(), d_n, recs.size() * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+    return hip_fail(ctx, e, "D2H");
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "sync");
+  // level-major across axes on the device -> per axis, level-major, 90-byte nodes
+  size_t level_off = 0;
+  uint32_t in_axis_off = 0;
+  for (uint32_t n = W; n >= 1; n /= 2) {
+    for (uint32_t a = 0; a < count; a++)
+      for (uint32_t j = 0; j < n; j++)
+        std::memcpy(nodes_out + ((size_t)a * (2 * W - 1) + in_axis_off + j) * kNode,
+                    &recs[(level_off + (size_t)a * n + j) * kNodeWords], kNode);
+    level_off += (size_t)count * n;
+    in_axis_off += n;
+    if (n == 1) break;
+  }
+  return CEL_OK;
+}
+
+cel_status cel_dah_tree(cel_ctx* ctx, const uint8_t* row_roots, const uint8_t* col_roots, uint32_t w,
+                        uint8_t* nodes_out) {
+  if (!ctx) return CEL_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (!row_roots || !col_roots || !nodes_out || !w) return fail(ctx, CEL_EINVAL, "nil argument");
+  const uint32_t n = 2 * w;
+  if (n & (n - 1)) return fail(ctx, CEL_ENOTPOW2, "DAH tree export needs a power-of-two root count");
+  DeviceGuard g(ctx->device);
+  hipError_t e = hipSuccess;
+  uint8_t* d_items = static_cast<uint8_t*>(scratch(ctx, S_IN, (size_t)n * kNode, &e));
+  void* d_w = scratch(ctx, S_WORK, merkle_workspace_size(n), &e);
+  uint32_t* d_l = static_cast<uint32_t*>(scratch(ctx, S_ROOTS, (size_t)(2 * n - 1) * 32, &e));
+  if (!d_items || !d_w || !d_l) return fail(ctx, CEL_ENOMEM, "device allocation failed");
+  hipStream_t s = ctx->stream;
+  if ((e = hipMemcpyAsync(d_items, row_roots, (size_t)w * kNode, hipMemcpyHostToDevice, s)) != hipSuccess ||
+      (e = hipMemcpyAsync(d_items + (size_t)w * kNode, col_roots, (size_t)w * kNode, hipMemcpyHostToDevice, s)) !=
+          hipSuccess)
+    return hip_fail(ctx, e, "H2D");
+  if ((e = launch_rfc_tree(d_items, n, d_l, d_w, s)) != hipSuccess) return hip_fail(ctx, e, "rfc tree");
+  std::vector<uint32_t> words((size_t)(2 * n - 1) * 8);
+  if ((e = hipMemcpyAsync(words.data(), d_l, words.size() * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+    return hip_fail(ctx, e, "D2H");
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "sync");
+  for (size_t i = 0; i < words.size(); i++) {  // big-endian words -> digest bytes
+    nodes_out[4 * i] = (uint8_t)(words[i] >> 24);
+    nodes_out[4 * i + 1] = (uint8_t)(words[i] >> 16);
+    nodes_out[4 * i + 2] = (uint8_t)(words[i] >> 8);
+    nodes_out[4 * i + 3] = (uint8_t)words[i];
+  }
+  return CEL_OK;
+}
+
 // ------------------------------------------------------------------- repair
 
 // rsmt2d Repair crossword loop. The control loop (which axes are solvable) runs

@@ -104,6 +104,14 @@ size_t axes_roots_workspace_size(uint32_t k, uint32_t naxes);
 hipError_t launch_axes_roots(const uint8_t* cells, uint32_t k, const int32_t* axis_idx, uint32_t naxes,
                              uint32_t* roots, void* work, hipStream_t s);
 
+// Exported trees (proofs): all NMT levels of gathered axes (level-major, 96-byte records,
+// axes_trees_nodes(k, naxes) records) and all RFC-6962 levels over n = 2^m 90-byte items
+// (2n - 1 nodes of 8 big-endian words; work: merkle_workspace_size(n) bytes).
+size_t axes_trees_nodes(uint32_t k, uint32_t naxes);
+hipError_t launch_axes_trees(const uint8_t* cells, uint32_t k, const int32_t* axis_idx, uint32_t naxes,
+                             uint32_t* nodes, hipStream_t s);
+hipError_t launch_rfc_tree(const uint8_t* items90, uint32_t n, uint32_t* levels, void* work, hipStream_t s);
+
 // Erasure decode of `naxes` axes of 2n shards each, gathered into a dense
 // [naxes][2n][len] buffer with a [naxes][2n] present mask. In place.
 hipError_t launch_rs_decode(uint8_t* shards, const uint8_t* present, uint32_t naxes, uint32_t n,

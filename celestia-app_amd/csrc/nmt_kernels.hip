@@ -866,4 +866,66 @@ hipError_t launch_merkle_root(const uint8_t* items, uint32_t n, uint32_t item_le
   return hipGetLastError();
 }
 
+// ---------------------------------------------------- exported trees (proofs, §8f)
+//
+// Every node of the NMT trees of `naxes` gathered axes (cells[a][2k][512], axis_idx[a]
+// = the row/column index that decides the Q0 namespace rule), level-major:
+//   nodes = level 0 [naxes][2k] | level 1 [naxes][k] | ... | level log2(2k) [naxes][1]
+// 96-byte records. This is what nmt ProveRange / the subtree-root cacher read instead
+// of rebuilding the trees on the CPU (pkg/proof/proof.go:151-201,
+// pkg/inclusion/nmt_caching.go:96-124).
+size_t axes_trees_nodes(uint32_t k, uint32_t naxes) { return (size_t)naxes * (4 * (size_t)k - 1); }
+
+hipError_t launch_axes_trees(const uint8_t* cells, uint32_t k, const int32_t* axis_idx, uint32_t naxes,
+                             uint32_t* nodes, hipStream_t s) {
+  const uint32_t W = 2 * k;
+  hipLaunchKernelGGL(k_axes_leaf, dim3((naxes * W + 255) / 256), dim3(256), 0, s, cells, k, axis_idx, naxes, nodes);
+  uint32_t nin = W;
+  uint32_t* src = nodes;
+  while (nin > 1) {
+    const uint32_t nout = nin / 2;
+    uint32_t* out = src + (size_t)naxes * nin * kNodeWords;
+    hipLaunchKernelGGL(k_level<false>, dim3((naxes * nout + 255) / 256, 1), dim3(256), 0, s, src, out, W, nin, naxes,
+                       nullptr, nullptr, nullptr);
+    src = out;
+    nin = nout;
+  }
+  return hipGetLastError();
+}
+
+// RFC-6962 tree of n = 2^m items of 90 bytes (DataAvailabilityHeader.Hash over
+// rowRoots || colRoots), every level: level 0 = the n leaf hashes SHA256(0x00 || item),
+// then n/2 inner hashes SHA256(0x01 || l || r), ..., the root. 8 big-endian words per
+// node. (merkle.ProofsFromByteSlices reads its aunts from these levels.)
+__global__ void k_rfc_leaves(const uint32_t* __restrict__ items, uint32_t n, uint32_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t R[kNodeWords], st[8];
+  load_node(items + (uint64_t)i * kNodeWords, R);
+  rfc_leaf90(R, st);
+  for (int j = 0; j < 8; j++) out[(uint64_t)i * 8 + j] = st[j];
+}
+
+__global__ void k_rfc_level(const uint32_t* __restrict__ in, uint32_t nout, uint32_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nout) return;
+  uint32_t st[8];
+  rfc_inner(in + (uint64_t)(2 * i) * 8, in + (uint64_t)(2 * i + 1) * 8, st);
+  for (int j = 0; j < 8; j++) out[(uint64_t)i * 8 + j] = st[j];
+}
+
+hipError_t launch_rfc_tree(const uint8_t* items90, uint32_t n, uint32_t* levels, void* work, hipStream_t s) {
+  if (!n || (n & (n - 1))) return hipErrorInvalidValue;
+  uint32_t* pad = static_cast<uint32_t*>(work);
+  hipLaunchKernelGGL(k_pad_items, dim3((n + 255) / 256), dim3(256), 0, s, items90, n, kNode, pad);
+  hipLaunchKernelGGL(k_rfc_leaves, dim3((n + 255) / 256), dim3(256), 0, s, pad, n, levels);
+  uint32_t* src = levels;
+  for (uint32_t m = n; m > 1; m /= 2) {
+    uint32_t* out = src + (size_t)m * 8;
+    hipLaunchKernelGGL(k_rfc_level, dim3((m / 2 + 255) / 256), dim3(256), 0, s, src, m / 2, out);
+    src = out;
+  }
+  return hipGetLastError();
+}
+
 }  // namespace cel

@@ -174,6 +174,33 @@ cel_status cel_repair(cel_ctx* ctx, uint8_t* eds, uint8_t* present, uint32_t k,
                       uint32_t share_size, const uint8_t* row_roots, const uint8_t* col_roots,
                       int32_t* bad_axis, int32_t* bad_index);
 
+/* ------------------------------------------------------- exported trees, proofs
+ * pkg/proof (proof.go:78-202, row_proof.go, share_proof.go) and the subtree-root
+ * cacher (pkg/inclusion/nmt_caching.go:96-124) need inner nodes, which the reference
+ * gets by rebuilding row trees on the CPU. Here the device hashes the trees and
+ * returns every node; proof building only selects nodes (host, no device).
+ *
+ * cel_axis_trees: all nodes of the NMTs of EDS axes [first, first + count) (axis 0 =
+ * rows, row i = cells (i, 0..2k-1); 1 = columns), eds = 2k*2k*share host bytes.
+ * nodes_out: count * (4k - 1) nodes of 90 B; per axis level-major from the 2k leaves
+ * up to the root (leaf j at [j], level-1 node j at [2k + j], ..., root last). */
+cel_status cel_axis_trees(cel_ctx* ctx, const uint8_t* eds, uint32_t k, uint32_t share_size,
+                          uint32_t axis, uint32_t first, uint32_t count, uint8_t* nodes_out);
+/* RFC-6962 tree over rowRoots || colRoots (w each, 2w a power of two), every level:
+ * nodes_out (4w - 1) * 32 B, level 0 = the 2w leaf hashes, ..., the root last (equal to
+ * cel_dah_hash). */
+cel_status cel_dah_tree(cel_ctx* ctx, const uint8_t* row_roots, const uint8_t* col_roots,
+                        uint32_t w, uint8_t* nodes_out);
+/* nmt ProveRange(start, end) on one tree of cel_axis_trees (nleaves = 2k): the proof
+ * nodes (90 B each, nmt order: maximal subtrees outside [start, end), left to right)
+ * to nodes_out (nullable: count only) and their count to *nnodes. */
+cel_status cel_nmt_prove_range(const uint8_t* tree_nodes, uint32_t nleaves, uint32_t start,
+                               uint32_t end, uint8_t* nodes_out, uint32_t* nnodes);
+/* merkle.ProofsFromByteSlices Aunts of item `index` (n items, a power of two) from a
+ * cel_dah_tree table: leaf sibling first, 32 B each, count to *naunts. */
+cel_status cel_merkle_aunts(const uint8_t* tree, uint32_t n, uint32_t index, uint8_t* aunts_out,
+                            uint32_t* naunts);
+
 /* ---------------------------------------------------- data-square construction
  * go-square v1.1.0 (host code, no device needed):
  *   greedy = 0: square.Construct (app/extend_block.go:16-25, app/process_proposal.go:121-130):
