@@ -269,7 +269,7 @@ def merkle_aunts(levels, n, index):
 def CreateShareToRowRootProofs(eds, start_row, end_row, start_leaf, end_leaf):
     """pkg/proof/proof.go:147-202 on device-built trees: per row, the nmt range proof of
     the selected shares and the raw shares."""
-    W = eds.Width()
+    k = eds.Width() // 2
     trees = axis_trees(eds, 0, start_row, end_row - start_row + 1)
     share_proofs, raw = [], []
     roots = eds.RowRoots()
@@ -277,7 +277,7 @@ def CreateShareToRowRootProofs(eds, start_row, end_row, start_leaf, end_leaf):
         if trees[i, -1].tobytes() != roots[r]:
             raise CelError(_lib.EINVAL, "eds row root is different than tree root")
         s = start_leaf if i == 0 else 0
-        e = end_leaf if r == end_row else W - 1
+        e = end_leaf if r == end_row else k - 1  # ODS part of the row (proof.go:180-183, squareSize = k)
         raw += [eds.GetCell(r, c) for c in range(s, e + 1)]
         share_proofs.append(NMTProof(Start=s, End=e + 1, Nodes=nmt_prove_range(trees[i], s, e + 1)))
     return share_proofs, raw
