@@ -28,7 +28,8 @@ EXPORTS = [
     "cel_codec_max_chunks", "cel_codec_name", "cel_codec_validate_chunk_size", "cel_axis_root",
     "cel_nmt_root", "cel_dah_hash", "cel_repair", "cel_dev_shard_workspace_size", "cel_dev_shard_rows",
     "cel_dev_shard_cols", "cel_dev_shard_finish", "cel_square_construct", "cel_square_last_error",
-    "cel_axis_trees", "cel_dah_tree", "cel_nmt_prove_range", "cel_merkle_aunts",
+    "cel_axis_trees", "cel_dah_tree", "cel_nmt_prove_range", "cel_merkle_aunts", "cel_commitment_paths",
+    "cel_get_commitment", "cel_subtree_root_coordinates",
 ]
 
 _lib = None
@@ -83,6 +84,9 @@ def load():
             "cel_dah_tree": (i32, [P, P, P, u32, P]),
             "cel_nmt_prove_range": (i32, [P, u32, u32, u32, P, P]),
             "cel_merkle_aunts": (i32, [P, u32, u32, P, P]),
+            "cel_commitment_paths": (i32, [u32, u32, u32, u32, P, P, P, u32, P]),
+            "cel_get_commitment": (i32, [P, P, u32, u32, u32, u32, u32, P]),
+            "cel_subtree_root_coordinates": (i32, [u32, u32, u32, u32, P, P, u32, P]),
         }
         for name, (res, args) in sigs.items():
             fn = getattr(l, name)

@@ -657,6 +657,44 @@ cel_status cel_dah_tree(cel_ctx* ctx, const uint8_t* row_roots, const uint8_t* c
   return CEL_OK;
 }
 
+cel_status cel_get_commitment(cel_ctx* ctx, const uint8_t* eds, uint32_t k, uint32_t share_size, uint32_t start,
+                              uint32_t blob_share_len, uint32_t subtree_root_threshold, uint8_t* commitment) {
+  if (!ctx) return CEL_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (!eds || !commitment || !blob_share_len || !subtree_root_threshold) return fail(ctx, CEL_EINVAL, "nil argument");
+  cel_status st = validate_square(ctx, k, share_size);
+  if (st) return st;
+  if ((uint64_t)start + blob_share_len > (uint64_t)k * k)  // get_commit.go:14-16
+    return fail(ctx, CEL_ETOOBIG, "cannot get commitment for blob that doesn't fit in square");
+  uint32_t n = 0;
+  if ((st = cel_commitment_paths(k, start, blob_share_len, subtree_root_threshold, nullptr, nullptr, nullptr, 0, &n)))
+    return fail(ctx, st, "commitment paths");
+  std::vector<uint32_t> rows(n), depths(n), pos(n);
+  cel_commitment_paths(k, start, blob_share_len, subtree_root_threshold, rows.data(), depths.data(), pos.data(), n,
+                       &n);
+  if (n > 2048) return fail(ctx, CEL_ETOOBIG, "too many subtree roots for the device merkle kernel");
+  const uint32_t r0 = rows.front(), nrows = rows.back() - r0 + 1, W = 2 * k;
+  DeviceGuard g(ctx->device);
+  hipError_t e = hipSuccess;
+  const size_t cells_b = (size_t)nrows * W * kShare;
+  uint8_t* d_c = static_cast<uint8_t*>(scratch(ctx, S_IN, cells_b, &e));
+  uint32_t* d_n = static_cast<uint32_t*>(scratch(ctx, S_WORK, axes_trees_nodes(k, nrows) * kNodeWords * 4, &e));
+  int32_t* d_idx = static_cast<int32_t*>(scratch(ctx, S_AUX, (size_t)(nrows + n) * 4, &e));
+  uint8_t* d_items = static_cast<uint8_t*>(scratch(ctx, S_ROOTS, (size_t)n * kNode + 64, &e));
+  void* d_mw = scratch(ctx, S_MASK, merkle_workspace_size(n), &e);
+  if (!d_c || !d_n || !d_idx || !d_items || !d_mw) return fail(ctx, CEL_ENOMEM, "device allocation failed");
+  uint8_t* d_out = d_items + (size_t)n * kNode + (64 - ((size_t)n * kNode) % 32) % 32;
+  hipStream_t s = ctx->stream;
+  if ((e = hipMemcpyAsync(d_c, eds + (size_t)r0 * W * kShare, cells_b, hipMemcpyHostToDevice, s)) != hipSuccess)
+    return hip_fail(ctx, e, "H2D");
+  if ((e = launch_commitment(d_c, k, r0, nrows, rows.data(), depths.data(), pos.data(), n, d_idx, d_n, d_items, d_mw,
+                             d_out, s)) != hipSuccess)
+    return hip_fail(ctx, e, "commitment");
+  if ((e = hipMemcpyAsync(commitment, d_out, 32, hipMemcpyDeviceToHost, s)) != hipSuccess) return hip_fail(ctx, e, "D2H");
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "sync");
+  return CEL_OK;
+}
+
 // ------------------------------------------------------------------- repair
 
 // rsmt2d Repair crossword loop. The control loop (which axes are solvable) runs

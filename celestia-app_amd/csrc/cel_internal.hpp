@@ -112,6 +112,14 @@ hipError_t launch_axes_trees(const uint8_t* cells, uint32_t k, const int32_t* ax
                              uint32_t* nodes, hipStream_t s);
 hipError_t launch_rfc_tree(const uint8_t* items90, uint32_t n, uint32_t* levels, void* work, hipStream_t s);
 
+hipError_t launch_gather_nodes(const uint32_t* nodes, const int32_t* rec, uint32_t n, uint8_t* out, hipStream_t s);
+// Blob share commitment (inclusion.cpp): trees of the gathered rows, subtree roots at
+// (rows[i], depths[i], positions[i]) of the rows' ODS halves, RFC-6962 root -> d_out[32].
+hipError_t launch_commitment(const uint8_t* d_cells, uint32_t k, uint32_t r0, uint32_t nrows, const uint32_t* rows,
+                             const uint32_t* depths, const uint32_t* positions, uint32_t npaths, int32_t* d_idx,
+                             uint32_t* d_nodes, uint8_t* d_items, void* d_merkle_work, uint8_t* d_out,
+                             hipStream_t s);
+
 // Erasure decode of `naxes` axes of 2n shards each, gathered into a dense
 // [naxes][2n][len] buffer with a [naxes][2n] present mask. In place.
 hipError_t launch_rs_decode(uint8_t* shards, const uint8_t* present, uint32_t naxes, uint32_t n,

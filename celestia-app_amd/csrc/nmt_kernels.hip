@@ -928,4 +928,18 @@ hipError_t launch_rfc_tree(const uint8_t* items90, uint32_t n, uint32_t* levels,
   return hipGetLastError();
 }
 
+// Pack selected 96-byte node records into 90-byte items: out[i] = nodes[rec[i]].
+__global__ void k_gather_nodes(const uint32_t* __restrict__ nodes, const int32_t* __restrict__ rec, uint32_t n,
+                               uint8_t* __restrict__ out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * kNode) return;
+  const uint32_t i = t / kNode, b = t % kNode;
+  out[t] = reinterpret_cast<const uint8_t*>(nodes + (uint64_t)rec[i] * kNodeWords)[b];
+}
+
+hipError_t launch_gather_nodes(const uint32_t* nodes, const int32_t* rec, uint32_t n, uint8_t* out, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_gather_nodes, dim3((n * kNode + 255) / 256), dim3(256), 0, s, nodes, rec, n, out);
+  return hipGetLastError();
+}
+
 }  // namespace cel

@@ -201,6 +201,27 @@ cel_status cel_nmt_prove_range(const uint8_t* tree_nodes, uint32_t nleaves, uint
 cel_status cel_merkle_aunts(const uint8_t* tree, uint32_t n, uint32_t index, uint8_t* aunts_out,
                             uint32_t* naunts);
 
+/* Blob share commitments from an EDS (pkg/inclusion).
+ * cel_commitment_paths: calculateCommitmentPaths (paths.go:16-47) for a blob of
+ * blob_share_len shares placed at the first aligned index >= start of a square of
+ * width square_size: per subtree root, its row and its (depth, position) inside the
+ * row's ODS half (the reference walk is WalkLeft then the depth bits of position,
+ * most significant first). n_out = count; arrays (nullable) hold up to cap entries.
+ * cel_get_commitment: GetCommitment (get_commit.go:12-30) over device-built row
+ * trees: the RFC-6962 root of those subtree roots (eds = 2k*2k*share host bytes). */
+cel_status cel_commitment_paths(uint32_t square_size, uint32_t start, uint32_t blob_share_len,
+                                uint32_t subtree_root_threshold, uint32_t* rows, uint32_t* depths,
+                                uint32_t* positions, uint32_t cap, uint32_t* n_out);
+/* calculateSubTreeRootCoordinates (paths.go:95-173): leaves [start, end) of a tree of
+ * depth max_depth covered left to right by the largest aligned subtrees of depth >=
+ * min_depth, as (depth, position) pairs. */
+cel_status cel_subtree_root_coordinates(uint32_t max_depth, uint32_t min_depth, uint32_t start,
+                                        uint32_t end, uint32_t* depths, uint32_t* positions,
+                                        uint32_t cap, uint32_t* n_out);
+cel_status cel_get_commitment(cel_ctx* ctx, const uint8_t* eds, uint32_t k, uint32_t share_size,
+                              uint32_t start, uint32_t blob_share_len,
+                              uint32_t subtree_root_threshold, uint8_t* commitment);
+
 /* ---------------------------------------------------- data-square construction
  * go-square v1.1.0 (host code, no device needed):
  *   greedy = 0: square.Construct (app/extend_block.go:16-25, app/process_proposal.go:121-130):
