@@ -101,6 +101,17 @@ class DataAvailabilityHeader:
     def SquareSize(self):
         return len(self.RowRoots) // 2
 
+    def ToProto(self):
+        """celestia.core.v1.da.DataAvailabilityHeader wire bytes
+        (proto/celestia/core/v1/da/data_availability_header.proto: 1 = repeated bytes
+        row_roots, 2 = repeated bytes column_roots; data_availability_header.go:110-119)."""
+        out = bytearray()
+        for tag, roots in ((0x0A, self.RowRoots), (0x12, self.ColumnRoots)):
+            for r in roots:
+                out.append(tag)
+                out += _uvarint(len(r)) + bytes(r)
+        return bytes(out)
+
     def ValidateBasic(self):
         if len(self.ColumnRoots) < MIN_EXTENDED_SQUARE_WIDTH or len(self.RowRoots) < MIN_EXTENDED_SQUARE_WIDTH:
             raise CelError(_lib.EINVAL, "minimum valid DataAvailabilityHeader has at least "
@@ -113,6 +124,50 @@ class DataAvailabilityHeader:
                                         f"{len(self.RowRoots)} col {len(self.ColumnRoots)}")
         if len(self.Hash()) != 32:
             raise CelError(_lib.EINVAL, f"wrong hash: expected size to be 32 bytes, got {len(self.Hash())} bytes")
+
+
+def _uvarint(n):
+    out = bytearray()
+    while True:
+        b = n & 0x7F
+        n >>= 7
+        out.append(b | (0x80 if n else 0))
+        if not n:
+            return bytes(out)
+
+
+def DataAvailabilityHeaderFromProto(buf):
+    """data_availability_header.go:121-131: decode, then ValidateBasic (raises CelError)."""
+    rows, cols, i = [], [], 0
+    buf = bytes(buf)
+    while i < len(buf):
+        key, i = _read_uvarint(buf, i)
+        if key & 7 != 2:
+            raise CelError(_lib.EINVAL, "proto: wrong wire type for DataAvailabilityHeader")
+        ln, i = _read_uvarint(buf, i)
+        if i + ln > len(buf):
+            raise CelError(_lib.EINVAL, "proto: unexpected EOF")
+        if key >> 3 == 1:
+            rows.append(buf[i:i + ln])
+        elif key >> 3 == 2:
+            cols.append(buf[i:i + ln])
+        i += ln
+    dah = DataAvailabilityHeader(rows, cols)
+    dah.ValidateBasic()
+    return dah
+
+
+def _read_uvarint(buf, i):
+    v, shift = 0, 0
+    while True:
+        if i >= len(buf) or shift > 63:
+            raise CelError(_lib.EINVAL, "proto: bad varint")
+        b = buf[i]
+        i += 1
+        v |= (b & 0x7F) << shift
+        if not b & 0x80:
+            return v, i
+        shift += 7
 
 
 def NilDataAvailabilityHeaderHash():

@@ -156,3 +156,37 @@ def test_extend_empty_block(ctx, golden):
     from celestia_eds import da, square
     eds = da.ExtendShares(list(square.Construct([])))
     assert da.NewDataAvailabilityHeader(eds).Hash().hex() == golden["dah_known_answers"]["min"]
+
+
+def test_dah_proto_conversion(ctx):
+    """TestDataAvailabilityHeaderProtoConversion (data_availability_header_test.go:101-133):
+    min and max (k = 128) DAHs survive ToProto / DataAvailabilityHeaderFromProto."""
+    from celestia_eds import da
+    big = da.NewDataAvailabilityHeader(da.ExtendShares(list(random_ods(128, 5).reshape(-1, 512))))
+    for dah in (da.MinDataAvailabilityHeader(), big):
+        res = da.DataAvailabilityHeaderFromProto(dah.ToProto())
+        assert res.RowRoots == dah.RowRoots and res.ColumnRoots == dah.ColumnRoots
+        assert res.Hash() == dah.Hash()
+    raw = da.MinDataAvailabilityHeader().ToProto()
+    assert raw[0] == 0x0A and raw[1] == 90 and raw[92] == 0x0A and raw[184] == 0x12  # 2 rows, then 2 columns
+
+
+def test_dah_validate_basic_cases(ctx):
+    """Test_DAHValidateBasic (data_availability_header_test.go:135-215)."""
+    from celestia_eds import CelError, da
+    big = da.NewDataAvailabilityHeader(da.ExtendShares(list(random_ods(128, 6).reshape(-1, 512))))
+    big.ValidateBasic()
+    da.MinDataAvailabilityHeader().ValidateBasic()
+    max_size = 128 * 128
+    too_big = da.DataAvailabilityHeader(big.RowRoots + [b"\x01" * 32] * (max_size - 256 + 1),
+                                        big.ColumnRoots + [b"\x01" * 32] * (max_size - 256 + 1))
+    too_small = da.DataAvailabilityHeader([b"\x02" * 32], [b"\x02" * 32])
+    bad_hash = da.MinDataAvailabilityHeader()
+    bad_hash.hash = bytes([1, 2, 3, 4])
+    mismatch = da.MinDataAvailabilityHeader()
+    mismatch.ColumnRoots = mismatch.ColumnRoots + [b"\x02" * 32]
+    for dah, msg in ((too_big, "maximum valid DataAvailabilityHeader has at most"),
+                     (too_small, "minimum valid DataAvailabilityHeader has at least"),
+                     (bad_hash, "wrong hash"), (mismatch, "unequal number of row and column roots")):
+        with pytest.raises(CelError, match=msg):
+            dah.ValidateBasic()
