@@ -178,3 +178,74 @@ func (cd Codec) Decode(shards [][]byte) ([][]byte, error) {
 	}
 	return out, nil
 }
+
+// SquareConstruct wraps cel_square_construct: go-square square.Construct (greedy =
+// false) or square.Build (greedy = true). It returns the ODS shares and, for Build,
+// which txs were kept. Host-only: no device work.
+func SquareConstruct(txs [][]byte, maxSquareSize, subtreeRootThreshold int, greedy bool) ([][]byte, []bool, error) {
+	total := 0
+	for _, t := range txs {
+		total += len(t)
+	}
+	buf := C.malloc(C.size_t(total + 1))
+	lens := C.malloc(C.size_t(4 * (len(txs) + 1)))
+	inc := C.malloc(C.size_t(len(txs) + 1))
+	defer C.free(buf)
+	defer C.free(lens)
+	defer C.free(inc)
+	b := unsafe.Slice((*byte)(buf), total+1)
+	l := unsafe.Slice((*C.uint32_t)(lens), len(txs)+1)
+	off := 0
+	for i, t := range txs {
+		copy(b[off:], t)
+		l[i] = C.uint32_t(len(t))
+		off += len(t)
+	}
+	g := C.uint32_t(0)
+	if greedy {
+		g = 1
+	}
+	var k C.uint32_t
+	st := C.cel_square_construct((*C.uint8_t)(buf), (*C.uint32_t)(lens), C.uint32_t(len(txs)),
+		C.uint32_t(maxSquareSize), C.uint32_t(subtreeRootThreshold), g, nil, 0, &k, (*C.uint8_t)(inc))
+	if st != 0 {
+		return nil, nil, fmt.Errorf("%s", C.GoString(C.cel_square_last_error()))
+	}
+	n := int(k) * int(k)
+	out := C.malloc(C.size_t(n * C.CEL_SHARE_SIZE))
+	defer C.free(out)
+	st = C.cel_square_construct((*C.uint8_t)(buf), (*C.uint32_t)(lens), C.uint32_t(len(txs)),
+		C.uint32_t(maxSquareSize), C.uint32_t(subtreeRootThreshold), g, (*C.uint8_t)(out), C.uint32_t(n), &k,
+		(*C.uint8_t)(inc))
+	if st != 0 {
+		return nil, nil, fmt.Errorf("%s", C.GoString(C.cel_square_last_error()))
+	}
+	o := unsafe.Slice((*byte)(out), n*C.CEL_SHARE_SIZE)
+	shares := make([][]byte, n)
+	for i := range shares {
+		shares[i] = append([]byte(nil), o[i*C.CEL_SHARE_SIZE:(i+1)*C.CEL_SHARE_SIZE]...)
+	}
+	kept := make([]bool, len(txs))
+	iv := unsafe.Slice((*byte)(inc), len(txs)+1)
+	for i := range kept {
+		kept[i] = iv[i] != 0
+	}
+	return shares, kept, nil
+}
+
+// GetCommitment wraps cel_get_commitment (pkg/inclusion.GetCommitment without the
+// EDSSubTreeRootCacher: the device hashes the rows' trees). eds: the flattened
+// 2k x 2k square.
+func (c *Context) GetCommitment(eds []byte, k, start, blobShareLen, subtreeRootThreshold int) ([]byte, error) {
+	buf := C.CBytes(eds)
+	defer C.free(buf)
+	out := make([]byte, 32)
+	c.mu.Lock()
+	defer c.mu.Unlock()
+	st := C.cel_get_commitment(c.ctx, (*C.uint8_t)(buf), C.uint32_t(k), C.CEL_SHARE_SIZE, C.uint32_t(start),
+		C.uint32_t(blobShareLen), C.uint32_t(subtreeRootThreshold), (*C.uint8_t)(unsafe.Pointer(&out[0])))
+	if err := c.err(st); err != nil {
+		return nil, err
+	}
+	return out, nil
+}
