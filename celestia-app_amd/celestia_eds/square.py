@@ -44,7 +44,7 @@ def _call(txs, max_square_size, subtree_root_threshold, greedy):
     st = run(out.ctypes.data_as(ctypes.c_void_p), n)
     if st != _lib.OK:
         raise _lib.CelError(st, l.cel_square_last_error().decode())
-    return out, [bool(included[i]) for i in range(len(txs))]
+    return out, [int(included[i]) for i in range(len(txs))]
 
 
 def Construct(txs, max_square_size=SQUARE_SIZE_UPPER_BOUND, subtree_root_threshold=SUBTREE_ROOT_THRESHOLD):
@@ -55,15 +55,6 @@ def Construct(txs, max_square_size=SQUARE_SIZE_UPPER_BOUND, subtree_root_thresho
 def Build(txs, max_square_size=SQUARE_SIZE_UPPER_BOUND, subtree_root_threshold=SUBTREE_ROOT_THRESHOLD):
     """-> (shares [k*k][512], kept txs: normal txs first, then blob txs)."""
     out, kept = _call(txs, max_square_size, subtree_root_threshold, 1)
-    normal, blob = [], []
-    for t, keep in zip(txs, kept):
-        if keep:
-            (blob if is_blob_tx(t) else normal).append(bytes(t))
+    normal = [bytes(t) for t, s in zip(txs, kept) if s == 1]
+    blob = [bytes(t) for t, s in zip(txs, kept) if s == 2]
     return out, normal + blob
-
-
-def is_blob_tx(tx):
-    """blob.UnmarshalBlobTx's verdict, through a one-tx greedy build (a blob tx lands in
-    the PFB namespace of the square)."""
-    out, kept = _call([tx], SQUARE_SIZE_UPPER_BOUND, SUBTREE_ROOT_THRESHOLD, 1)
-    return bool(kept[0]) and bytes(out[0][:29]) == bytes(28) + b"\x04"

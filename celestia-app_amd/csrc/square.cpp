@@ -437,7 +437,8 @@ cel_status cel_square_construct(const uint8_t* txs, const uint32_t* tx_lens, uin
     const uint8_t* inner;
     size_t inner_len;
     bool ok;
-    if (unmarshal_blob_tx(tx, n, inner, inner_len, blobs)) {
+    const bool is_blob = unmarshal_blob_tx(tx, n, inner, inner_len, blobs);
+    if (is_blob) {
       seen_blob_tx = true;
       ok = b.append_blob_tx(inner, inner_len, blobs);
     } else {
@@ -447,7 +448,7 @@ cel_status cel_square_construct(const uint8_t* txs, const uint32_t* tx_lens, uin
       }
       ok = b.append_tx(tx, n);
     }
-    if (included) included[i] = ok ? 1 : 0;
+    if (included) included[i] = ok ? (is_blob ? 2 : 1) : 0;
     if (!ok && !greedy) {
       g_square_error = std::string("not enough space to append ") + (seen_blob_tx ? "blob tx" : "tx") +
                        " at index " + std::to_string(i);

@@ -228,7 +228,7 @@ func SquareConstruct(txs [][]byte, maxSquareSize, subtreeRootThreshold int, gree
 	kept := make([]bool, len(txs))
 	iv := unsafe.Slice((*byte)(inc), len(txs)+1)
 	for i := range kept {
-		kept[i] = iv[i] != 0
+		kept[i] = iv[i] != 0 // 1 = normal tx kept, 2 = blob tx kept
 	}
 	return shares, kept, nil
 }

@@ -229,8 +229,9 @@ cel_status cel_get_commitment(cel_ctx* ctx, const uint8_t* eds, uint32_t k, uint
  *               (CEL_ETOOBIG "not enough space to append tx at index i",
  *               CEL_EINVAL "normal transaction at index i can not be appended after blob tx");
  *   greedy = 1: square.Build (app/prepare_proposal.go:48-61): txs that do not fit are
- *               skipped; included[i] (nullable, ntx bytes) reports which were kept
- *               (the square orders kept normal txs before kept blob txs).
+ *               skipped (the square orders kept normal txs before kept blob txs).
+ * included (nullable, ntx bytes): 0 = tx not in the square, 1 = normal tx kept,
+ * 2 = blob tx kept.
  * txs: the ntx transactions concatenated, tx_lens[ntx] their lengths.
  * max_square_size / subtree_root_threshold: appconsts SquareSizeUpperBound (128) and
  * SubtreeRootThreshold (64) (pkg/appconsts/v1,v2/app_consts.go).
