@@ -308,3 +308,19 @@ def NewShareInclusionProof(ods_shares, namespace, share_start, share_end):
     """pkg/proof/proof.go:64-76: extend the ODS on the device, then prove."""
     from . import da
     return NewShareInclusionProofFromEDS(da.ExtendShares(ods_shares), namespace, share_start, share_end)
+
+
+TX_NAMESPACE = bytes(28) + b"\x01"
+PFB_NAMESPACE = bytes(28) + b"\x04"
+
+
+def NewTxInclusionProof(txs, tx_index, max_square_size=128, subtree_root_threshold=64):
+    """pkg/proof/proof.go:21-48: square.Construct, FindTxShareRange, then the share proof
+    of that range in the tx's namespace (PayForBlob for blob txs, proof.go:50-56)."""
+    from . import square
+    if tx_index >= len(txs):
+        raise CelError(_lib.EINVAL, f"txIndex {tx_index} out of bounds")
+    start, end = square.TxShareRange(txs, tx_index, max_square_size, subtree_root_threshold)
+    ods = square.Construct(txs, max_square_size, subtree_root_threshold)
+    ns = PFB_NAMESPACE if bytes(ods[start][:NS]) == PFB_NAMESPACE else TX_NAMESPACE
+    return NewShareInclusionProof(list(ods), ns, start, end)

@@ -334,6 +334,7 @@ struct Builder {
   std::vector<Bytes> txs;
   std::vector<Pfb> pfbs;
   std::vector<Element> blobs;
+  std::vector<Bytes> iws;  // final PFB index wrappers (after export_square)
 
   Builder(uint32_t m, uint32_t t) : max_size(m), threshold(t), max_capacity((uint64_t)m * m) {}
 
@@ -390,7 +391,7 @@ struct Builder {
       cursor += e.shares;
       end_of_last = cursor;
     }
-    std::vector<Bytes> iws;
+    iws.clear();
     for (const Pfb& p : pfbs) iws.push_back(marshal_index_wrapper(p.tx, p.len, p.idx));
     write_compact(kTxNs, txs, sq);
     write_compact(kPfbNs, iws, sq);
@@ -401,6 +402,26 @@ struct Builder {
     const uint32_t have = (uint32_t)(sq.size() / kShare);
     write_padding(tail_pad_ns(), (uint32_t)((uint64_t)k * k - have), sq);
     return k;
+  }
+
+  // Builder.FindTxShareRange (after export_square): the shares [start, end) holding the
+  // uvarint(len) || tx unit of normal tx `i` (i < txs.size()) or of the PFB index
+  // wrapper i - txs.size() (offset by the tx shares, which precede the PFB shares).
+  bool tx_range(size_t i, uint32_t& start, uint32_t& end) const {
+    const bool pfb = i >= txs.size();
+    const std::vector<Bytes>& units = pfb ? iws : txs;
+    const size_t u = pfb ? i - txs.size() : i;
+    if (u >= units.size()) return false;
+    uint64_t off = 0;
+    for (size_t j = 0; j < u; j++) off += uvarint_len(units[j].size()) + units[j].size();
+    const uint64_t last = off + uvarint_len(units[u].size()) + units[u].size() - 1;
+    auto share_of = [](uint64_t b) -> uint32_t {
+      return b < kCompactFirst ? 0u : 1u + (uint32_t)((b - kCompactFirst) / kCompactCont);
+    };
+    const uint32_t base = pfb ? compact_shares_for(tx_bytes) : 0u;
+    start = base + share_of(off);
+    end = base + share_of(last) + 1;
+    return true;
   }
 };
 
@@ -416,17 +437,14 @@ extern "C" {
 
 const char* cel_square_last_error(void) { return g_square_error.c_str(); }
 
-cel_status cel_square_construct(const uint8_t* txs, const uint32_t* tx_lens, uint32_t ntx, uint32_t max_square_size,
-                                uint32_t subtree_root_threshold, uint32_t greedy, uint8_t* shares_out,
-                                uint32_t cap_shares, uint32_t* k_out, uint8_t* included) {
+}  // extern "C"
+
+namespace {
+
+// NewBuilder(txs...) / Build's admission loop; fills included[] (0 / 1 normal / 2 blob).
+cel_status build_square(cel::sq::Builder& b, const uint8_t* txs, const uint32_t* tx_lens, uint32_t ntx,
+                        uint32_t greedy, uint8_t* included) {
   using namespace cel::sq;
-  g_square_error.clear();
-  if ((ntx && (!txs || !tx_lens)) || !k_out || !max_square_size || !subtree_root_threshold ||
-      (max_square_size & (max_square_size - 1))) {
-    g_square_error = "invalid argument";
-    return CEL_EINVAL;
-  }
-  Builder b(max_square_size, subtree_root_threshold);
   size_t off = 0;
   bool seen_blob_tx = false;
   std::vector<Blob> blobs;
@@ -455,6 +473,31 @@ cel_status cel_square_construct(const uint8_t* txs, const uint32_t* tx_lens, uin
       return CEL_ETOOBIG;
     }
   }
+  return CEL_OK;
+}
+
+bool args_ok(const uint8_t* txs, const uint32_t* tx_lens, uint32_t ntx, uint32_t max_square_size,
+             uint32_t subtree_root_threshold) {
+  return !((ntx && (!txs || !tx_lens)) || !max_square_size || !subtree_root_threshold ||
+           (max_square_size & (max_square_size - 1)));
+}
+
+}  // namespace
+
+extern "C" {
+
+cel_status cel_square_construct(const uint8_t* txs, const uint32_t* tx_lens, uint32_t ntx, uint32_t max_square_size,
+                                uint32_t subtree_root_threshold, uint32_t greedy, uint8_t* shares_out,
+                                uint32_t cap_shares, uint32_t* k_out, uint8_t* included) {
+  using namespace cel::sq;
+  g_square_error.clear();
+  if (!k_out || !args_ok(txs, tx_lens, ntx, max_square_size, subtree_root_threshold)) {
+    g_square_error = "invalid argument";
+    return CEL_EINVAL;
+  }
+  Builder b(max_square_size, subtree_root_threshold);
+  cel_status st = build_square(b, txs, tx_lens, ntx, greedy, included);
+  if (st) return st;
   std::vector<uint8_t> sq;
   const uint32_t k = b.export_square(sq);
   *k_out = k;
@@ -465,6 +508,30 @@ cel_status cel_square_construct(const uint8_t* txs, const uint32_t* tx_lens, uin
     return CEL_EINVAL;
   }
   std::memcpy(shares_out, sq.data(), sq.size());
+  return CEL_OK;
+}
+
+cel_status cel_square_tx_range(const uint8_t* txs, const uint32_t* tx_lens, uint32_t ntx, uint32_t max_square_size,
+                               uint32_t subtree_root_threshold, uint32_t tx_index, uint32_t* start, uint32_t* end) {
+  using namespace cel::sq;
+  g_square_error.clear();
+  if (!start || !end || !args_ok(txs, tx_lens, ntx, max_square_size, subtree_root_threshold)) {
+    g_square_error = "invalid argument";
+    return CEL_EINVAL;
+  }
+  if (tx_index >= ntx) {  // pkg/proof/proof.go:23-25
+    g_square_error = "txIndex " + std::to_string(tx_index) + " out of bounds";
+    return CEL_EINVAL;
+  }
+  Builder b(max_square_size, subtree_root_threshold);
+  cel_status st = build_square(b, txs, tx_lens, ntx, 0, nullptr);
+  if (st) return st;
+  std::vector<uint8_t> sq;
+  b.export_square(sq);
+  if (!b.tx_range(tx_index, *start, *end)) {
+    g_square_error = "txIndex " + std::to_string(tx_index) + " out of range";
+    return CEL_EINVAL;
+  }
   return CEL_OK;
 }
 

@@ -241,7 +241,13 @@ cel_status cel_square_construct(const uint8_t* txs, const uint32_t* tx_lens, uin
                                 uint32_t max_square_size, uint32_t subtree_root_threshold,
                                 uint32_t greedy, uint8_t* shares_out, uint32_t cap_shares,
                                 uint32_t* k_out, uint8_t* included);
-/* Message of the last cel_square_construct failure on this thread. */
+/* go-square Builder.FindTxShareRange after Construct (pkg/proof/proof.go:21-48,
+ * NewTxInclusionProof): the ODS shares [*start, *end) holding tx `tx_index` (a normal tx,
+ * or the index wrapper of a blob tx, which lives in the PayForBlob namespace). */
+cel_status cel_square_tx_range(const uint8_t* txs, const uint32_t* tx_lens, uint32_t ntx,
+                               uint32_t max_square_size, uint32_t subtree_root_threshold,
+                               uint32_t tx_index, uint32_t* start, uint32_t* end);
+/* Message of the last cel_square_construct / cel_square_tx_range failure on this thread. */
 const char* cel_square_last_error(void);
 
 #ifdef __cplusplus

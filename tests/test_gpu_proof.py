@@ -87,3 +87,16 @@ def test_exported_trees_match_roots(ctx):
             assert t[off + n + j].tobytes() == _nmt_node(t[off + 2 * j].tobytes(), t[off + 2 * j + 1].tobytes())
         off += n
         n //= 2
+
+
+def test_tx_inclusion_proofs_block408(ctx, golden):
+    """NewTxInclusionProof (pkg/proof/proof.go:21-48) for normal and blob txs of block 408
+    verifies against the block's data root."""
+    from celestia_eds import proof, square
+    txs = block408_txs()
+    root = bytes.fromhex(golden["block408"]["data_hash"])
+    n_normal = sum(1 for t in txs if not square.is_blob_tx(t))
+    for i in (0, n_normal - 1, n_normal, len(txs) - 1):
+        p = proof.NewTxInclusionProof(txs, i)
+        p.Validate(root)
+        assert p.NamespaceId[-1] == (0x01 if i < n_normal else 0x04)

@@ -96,3 +96,39 @@ def test_worst_case_square_fits_max():
     assert ods.shape[0] <= 128 * 128 and len(kept) >= 1
     k, ref = _oracle_square(kept)
     assert np.array_equal(ods, ref)
+
+
+def _compact_payload(shares):
+    """Concatenated data bytes of a run of compact shares (shares.md:24-98 headers)."""
+    out = b""
+    for i, s in enumerate(shares):
+        s = bytes(s)
+        head = 29 + 1 + (4 if s[29] & 1 else 0) + 4
+        out += s[head:]
+    return out
+
+
+def test_tx_share_ranges_block408():
+    """Builder.FindTxShareRange: every tx of block 408 (normal txs and the index wrappers
+    of blob txs) lies inside the compact shares its range names."""
+    from celestia_eds import square
+    txs = block408_txs()
+    ods = square.Construct(txs)
+    n_normal = sum(1 for t in txs if not square.is_blob_tx(t))
+    prev_end = 0
+    for i in (0, 1, n_normal // 2, n_normal - 1, n_normal, len(txs) - 1):
+        s, e = square.TxShareRange(txs, i)
+        assert 0 <= s < e <= len(ods)
+        ns = bytes(ods[s][:29])
+        assert ns == bytes(28) + (b"\x01" if i < n_normal else b"\x04")
+        payload = _compact_payload(ods[s:e])
+        if i < n_normal:
+            assert txs[i] in payload
+        else:  # the IndexWrapper embeds the inner tx of the BlobTx
+            assert b"INDX" in payload
+        if i < n_normal:
+            assert s >= prev_end - 1
+            prev_end = e
+    from celestia_eds import CelError
+    with pytest.raises(CelError, match="txIndex 274 out of bounds"):
+        square.TxShareRange(txs, len(txs))
