@@ -58,3 +58,26 @@ def Build(txs, max_square_size=SQUARE_SIZE_UPPER_BOUND, subtree_root_threshold=S
     normal = [bytes(t) for t, s in zip(txs, kept) if s == 1]
     blob = [bytes(t) for t, s in zip(txs, kept) if s == 2]
     return out, normal + blob
+
+
+def TxShareRange(txs, tx_index, max_square_size=SQUARE_SIZE_UPPER_BOUND,
+                 subtree_root_threshold=SUBTREE_ROOT_THRESHOLD):
+    """Builder.FindTxShareRange after square.Construct(txs): (start, end) ODS shares of tx
+    `tx_index` (its PFB index wrapper for a blob tx)."""
+    l = _lib.load()
+    txs = [bytes(t) for t in txs]
+    lens = (ctypes.c_uint32 * max(len(txs), 1))(*[len(t) for t in txs])
+    blob = b"".join(txs)
+    buf = ctypes.create_string_buffer(blob, max(len(blob), 1))
+    a, b = ctypes.c_uint32(), ctypes.c_uint32()
+    st = l.cel_square_tx_range(buf, lens, len(txs), max_square_size, subtree_root_threshold, tx_index,
+                               ctypes.byref(a), ctypes.byref(b))
+    if st != _lib.OK:
+        raise _lib.CelError(st, l.cel_square_last_error().decode())
+    return a.value, b.value
+
+
+def is_blob_tx(tx):
+    """blob.UnmarshalBlobTx's verdict, read from a one-tx square.Build (included code 2 =
+    kept blob tx; a blob tx too large for a 128 x 128 square reads as not kept)."""
+    return _call([tx], SQUARE_SIZE_UPPER_BOUND, SUBTREE_ROOT_THRESHOLD, 1)[1][0] == 2
