@@ -294,20 +294,13 @@ struct Perm16 {
   uint32_t t[kTw16Words];
 };
 
-// One product table into VGPRs: five 16-byte vector loads from an address every lane
-// shares (an L1/L2 broadcast). Scalar loads would put 20 SGPRs per live table under
-// pressure, and gfx950 VOP3 reads at most one SGPR, so v_perm needs VGPR tables anyway.
-// `dep` is the last value the previous butterfly block wrote: a fake data dependency
-// that pins the load after that block (otherwise the DAG scheduler issues every table
-// load of a phase up front and spills them).
-__device__ __forceinline__ Perm16 load_tab16(const uint32_t* __restrict__ tw, int idx, uint32_t dep) {
-  uint32_t off = (uint32_t)idx * (kTw16Words * 4);
-  asm volatile("" : "+v"(off) : "v"(dep));
-  const uint4* p = reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(tw) + off);
+// One product table from LDS (wave-uniform address: a broadcast read, ~LDS latency instead
+// of an L2 round trip per twiddle group).
+__device__ __forceinline__ Perm16 lds_tab16(const uint32_t* p) {
   Perm16 r;
 #pragma unroll
   for (int i = 0; i < (int)kTw16Words / 4; i++) {
-    const uint4 v = p[i];
+    const uint4 v = reinterpret_cast<const uint4*>(p)[i];
     r.t[4 * i] = v.x;
     r.t[4 * i + 1] = v.y;
     r.t[4 * i + 2] = v.z;
@@ -351,9 +344,23 @@ __global__ __launch_bounds__(64 * (1 << (LOGK - 5))) void k_rs_encode_gf16p(RsGe
   constexpr int LOGS = 5;
   constexpr int G = K / S;
   constexpr int L = S / G;
-  extern __shared__ uint32_t lds[];  // [K][64] dwords: one half (lo or hi) of the image
+  // LDS: [K][64] dwords = one half (lo or hi) of the exchange image, then the 2(G-1)
+  // product tables of the B layers. While the image is not in use (before the first
+  // exchange, after the second) its space holds each wave's 31 A-layer tables, staged
+  // with one bulk load: table reads in the A layers cost an LDS round trip, not a
+  // dependent L2 load per twiddle group (which left the kernel 43 % memory-wait bound).
+  extern __shared__ uint32_t lds[];
+  constexpr int TW = (int)kTw16Words;
+  uint32_t* const btab = lds + K * 64;  // [2][G-1][TW]
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint32_t* const atab = lds + wv * 31 * TW;  // this wave's A tables, table m - 1 for m = 1..31
+  // stage: A tables of the IFFT (skew K-1 + wv*S + m) and all B tables
+  for (int i = lane; i < 31 * TW; i += 64) atab[i] = tw[(K - 1 + wv * S + 1) * TW + i];
+  for (int i = threadIdx.x; i < 2 * (G - 1) * TW; i += blockDim.x) {
+    const int tb = i / TW, dir = tb / (G - 1), m = tb % (G - 1) + 1;
+    btab[i] = tw[(dir == 0 ? K - 1 + S * m : S * m - 1) * TW + i % TW];
+  }
   // every lane is active: the launcher requires len % 512 == 0
   const uint32_t col = blockIdx.y * 512u + (uint32_t)(lane >> 3) * 64u + (uint32_t)(lane & 7) * 4u;
   // buffer resources: scalar base per (square, axis), 32-bit lane offset, scalar shard offset
@@ -384,14 +391,14 @@ __global__ __launch_bounds__(64 * (1 << (LOGK - 5))) void k_rs_encode_gf16p(RsGe
       __builtin_amdgcn_raw_buffer_store_b32(wh[i], rdc, col + 32, so, 0);
     }
   }
-  uint32_t last = wh[S - 1];
+  __syncthreads();  // staged tables visible
   // IFFT, arrangement A (D < S): twiddle from the wave's group only
 #pragma unroll
   for (int lg = 0; lg < LOGS; lg++) {
     const int D = 1 << lg;
 #pragma unroll
     for (int base = 0; base < S; base += 2 * D) {
-      const Perm16 t = load_tab16(tw, K - 1 + wv * S + base + D, last);
+      const Perm16 t = lds_tab16(atab + (base + D - 1) * TW);
 #pragma unroll
       for (int j = 0; j < D; j++) {
         pin2(wl[base + j], wh[base + j], wl[base + j + D], wh[base + j + D]);
@@ -400,7 +407,6 @@ __global__ __launch_bounds__(64 * (1 << (LOGK - 5))) void k_rs_encode_gf16p(RsGe
         gf16_muladd4(wl[base + j], wh[base + j], wl[base + j + D], wh[base + j + D], t);
         opaque(wl[base + j]);
         opaque(wh[base + j]);
-        last = wh[base + j];
         __builtin_amdgcn_sched_barrier(0);
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -425,15 +431,15 @@ __global__ __launch_bounds__(64 * (1 << (LOGK - 5))) void k_rs_encode_gf16p(RsGe
       __syncthreads();
     }
   };
+  __syncthreads();  // every wave done with its A tables before the image overwrites them
   exchange(true);
-  last = wh[S - 1];
   // IFFT, arrangement B (D = S << t): pairs (h, h + 2^t), twiddle from h only
 #pragma unroll
   for (int t = 0; (1 << t) < G; t++) {
     const int dh = 1 << t;
 #pragma unroll
     for (int hb = 0; hb < G; hb += 2 * dh) {
-      const Perm16 tb = load_tab16(tw, K - 1 + S * hb + S * dh, last);
+      const Perm16 tb = lds_tab16(btab + (hb + dh - 1) * TW);
 #pragma unroll
       for (int h = hb; h < hb + dh; h++)
 #pragma unroll
@@ -445,7 +451,6 @@ __global__ __launch_bounds__(64 * (1 << (LOGK - 5))) void k_rs_encode_gf16p(RsGe
           gf16_muladd4(wl[x], wh[x], wl[y], wh[y], tb);
           opaque(wl[x]);
           opaque(wh[x]);
-          last = wh[x];
           __builtin_amdgcn_sched_barrier(0);
         }
       __builtin_amdgcn_sched_barrier(0);
@@ -457,7 +462,7 @@ __global__ __launch_bounds__(64 * (1 << (LOGK - 5))) void k_rs_encode_gf16p(RsGe
     const int dh = G >> (t + 1);
 #pragma unroll
     for (int hb = 0; hb < G; hb += 2 * dh) {
-      const Perm16 tb = load_tab16(tw, S * hb + S * dh - 1, last);
+      const Perm16 tb = lds_tab16(btab + ((G - 1) + hb + dh - 1) * TW);
 #pragma unroll
       for (int h = hb; h < hb + dh; h++)
 #pragma unroll
@@ -471,21 +476,21 @@ __global__ __launch_bounds__(64 * (1 << (LOGK - 5))) void k_rs_encode_gf16p(RsGe
           wh[y] ^= wh[x];
           opaque(wl[y]);
           opaque(wh[y]);
-          last = wh[y];
           __builtin_amdgcn_sched_barrier(0);
         }
       __builtin_amdgcn_sched_barrier(0);
     }
   }
-  exchange(false);
-  last = wh[S - 1];
+  exchange(false);  // ends with a barrier: the image space is free again
+  for (int i = lane; i < 31 * TW; i += 64) atab[i] = tw[(wv * S) * TW + i];  // FFT A: skew wv*S + m - 1
+  __syncthreads();
   // FFT, arrangement A
 #pragma unroll
   for (int lg = LOGS - 1; lg >= 0; lg--) {
     const int D = 1 << lg;
 #pragma unroll
     for (int base = 0; base < S; base += 2 * D) {
-      const Perm16 t = load_tab16(tw, wv * S + base + D - 1, last);
+      const Perm16 t = lds_tab16(atab + (base + D - 1) * TW);
 #pragma unroll
       for (int j = 0; j < D; j++) {
         pin2(wl[base + j], wh[base + j], wl[base + j + D], wh[base + j + D]);
@@ -496,7 +501,6 @@ __global__ __launch_bounds__(64 * (1 << (LOGK - 5))) void k_rs_encode_gf16p(RsGe
         wh[base + j + D] ^= wh[base + j];
         opaque(wl[base + j + D]);
         opaque(wh[base + j + D]);
-        last = wh[base + j + D];
         __builtin_amdgcn_sched_barrier(0);
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -517,7 +521,7 @@ template <int LOGK>
 static hipError_t launch_gf16p(const RsGeom& g, const DeviceTables& t, hipStream_t s) {
   constexpr int K = 1 << LOGK;
   constexpr int threads = 64 * (K / 32);
-  const size_t lds = (size_t)K * 64 * 4;
+  const size_t lds = ((size_t)K * 64 + 2 * (K / 32 - 1) * kTw16Words) * 4;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)k_rs_encode_gf16p<LOGK>,
