@@ -35,14 +35,16 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table)
 # per wave: 1024 SIMDs x 2.4 GHz x 64 / 4528 = 34.7 G compressions/s.
 SHA_MIX_CEILING = 1024 * 2.4e9 * 64 / 4528
 # Measured HBM traffic of the RS extension (rocprofv3 FETCH_SIZE/WRITE_SIZE passes).
-TRAFFIC_PROFILE = os.path.join(ROOT, "profiles", "r1_rs_traffic.json")
+# (input layout -> profile): ODS in Q0 of the EDS (in place) / separate ODS buffer.
+TRAFFIC_PROFILE = {"eds": "r1_rs_traffic_inplace.json", "ods": "r1_rs_traffic.json"}
 
 
-def _rs_traffic(k, batch):
+def _rs_traffic(k, batch, layout):
     """HBM bytes per RS launch pair from the committed PMC profile, scaled to `batch`
     squares (per-square traffic is batch-independent at these sizes), or None."""
+    name = TRAFFIC_PROFILE[layout]
     try:
-        with open(TRAFFIC_PROFILE) as f:
+        with open(os.path.join(ROOT, "profiles", name)) as f:
             p = json.load(f)
     except (OSError, ValueError):
         return None
@@ -50,7 +52,7 @@ def _rs_traffic(k, batch):
         return None
     return {"bytes": p["bytes_per_square"] * batch, "per_square": p["bytes_per_square"],
             "vs_algorithmic": p["bytes_per_square"] / p["algorithmic_bytes_per_square"],
-            "source": "profiles/r1_rs_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, KiB)"}
+            "source": f"profiles/{name} (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, KiB)"}
 
 
 def parse():
@@ -63,6 +65,9 @@ def parse():
     ap.add_argument("--distinct", type=int, default=4, help="distinct synthetic squares per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--input", default="eds", choices=["eds", "ods"],
+                    help="eds: the upload places each ODS in Q0 of its EDS buffer and the extension "
+                         "reads it in place; ods: separate contiguous ODS buffer, the row pass copies Q0")
     ap.add_argument("--phase-reps", type=int, default=10)
     ap.add_argument("--mode", default="batch", choices=["batch", "sharded", "repair"],
                     help="batch: independent squares per GPU (configs 2, 4); sharded: one square "
@@ -272,10 +277,10 @@ def main():
 
     ctx = default_context(local)
     k, B = a.k, a.batch
-    sb = SquareBatch(B, k, device=local, ctx=ctx)
+    sb = SquareBatch(B, k, device=local, ctx=ctx, ods_in_eds=(a.input == "eds"))
     distinct = [random_ods(k, 1_000_003 * rank + i) for i in range(min(a.distinct, B))]
     host = np.stack([distinct[i % len(distinct)] for i in range(B)])
-    sb.ods.copy_(torch.from_numpy(host))
+    sb.load_ods(torch.from_numpy(host))
     torch.cuda.synchronize()
 
     def barrier():
@@ -348,6 +353,8 @@ def main():
             "share_size": 512,
             "field": "GF(2^8)" if 2 * k <= 256 else "GF(2^16)",
             "parallelism": f"batch{world}",
+            "input_layout": ("ODS in Q0 of the EDS buffer (placed by the upload)" if a.input == "eds"
+                             else "contiguous ODS buffer"),
         },
         "roofline": {
             "bound": "hbm",
@@ -357,7 +364,7 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": rs_gbs / HBM_PEAK_GBS,
-            "traffic": _rs_traffic(k, B),
+            "traffic": _rs_traffic(k, B, a.input),
             "avg_launch_us": t_ext * 1e6,
         },
         "roofline_nmt": {

@@ -202,6 +202,26 @@ static cel_status validate_square(cel_ctx* ctx, uint32_t k, uint32_t share_size)
   return CEL_OK;
 }
 
+// n row-major k x k ODSs (host or device memory) -> Q0 of n row-major 2k x 2k EDSs.
+static hipError_t place_ods(const void* src, uint32_t n, uint32_t k, void* d_eds, hipStream_t s) {
+  const size_t w = (size_t)k * kShare, sq_ods = (size_t)k * w, sq_eds = 4 * sq_ods;
+  for (uint32_t i = 0; i < n; i++) {
+    const hipError_t e = hipMemcpy2DAsync(static_cast<uint8_t*>(d_eds) + i * sq_eds, 2 * w,
+                                          static_cast<const uint8_t*>(src) + i * sq_ods, w, w, k, hipMemcpyDefault, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+cel_status cel_dev_place_ods(cel_ctx* ctx, const void* ods, uint32_t n, uint32_t k, void* d_eds, void* stream) {
+  if (!ctx || !ods || !d_eds || !n) return CEL_EINVAL;
+  cel_status st = validate_square(ctx, k, kShare);
+  if (st) return st;
+  DeviceGuard g(ctx->device);
+  const hipError_t e = place_ods(ods, n, k, d_eds, pick_stream(ctx, stream));
+  return e == hipSuccess ? CEL_OK : hip_fail(ctx, e, "place ods");
+}
+
 cel_status cel_dev_extend_only(cel_ctx* ctx, const void* d_ods, uint32_t n, uint32_t k, void* d_eds, void* stream) {
   if (!ctx || !d_eds || !n) return CEL_EINVAL;
   cel_status st = validate_square(ctx, k, kShare);
@@ -270,8 +290,6 @@ cel_status cel_extend_batch(cel_ctx* ctx, const uint8_t* ods, uint32_t n, uint32
   const size_t ods_b = (size_t)n * k * k * kShare, eds_b = 4 * ods_b;
   const size_t roots_b = (size_t)n * 2 * k * kNode;
   hipError_t e = hipSuccess;
-  uint8_t* d_ods = static_cast<uint8_t*>(scratch(ctx, S_IN, ods_b, &e));
-  if (!d_ods) return fail(ctx, CEL_ENOMEM, "device allocation failed");
   uint8_t* d_eds = static_cast<uint8_t*>(scratch(ctx, S_EDS, eds_b, &e));
   if (!d_eds) return fail(ctx, CEL_ENOMEM, "device allocation failed");
   void* d_work = scratch(ctx, S_WORK, cel_dev_workspace_size(k, n), &e);
@@ -283,8 +301,9 @@ cel_status cel_extend_batch(cel_ctx* ctx, const uint8_t* ods, uint32_t n, uint32
   uint8_t* d_dah = d_out + 2 * roots_b;
   int32_t* d_st = reinterpret_cast<int32_t*>(d_out + 2 * roots_b + (size_t)n * 32);
   hipStream_t s = ctx->stream;
-  if ((e = hipMemcpyAsync(d_ods, ods, ods_b, hipMemcpyHostToDevice, s)) != hipSuccess) return hip_fail(ctx, e, "H2D");
-  st = cel_dev_extend_batch(ctx, d_ods, n, k, d_eds, d_rr, d_cr, d_dah, d_st, d_work, s, flags);
+  // the upload places every ODS in Q0 of its EDS; the extension reads it in place
+  if ((e = place_ods(ods, n, k, d_eds, s)) != hipSuccess) return hip_fail(ctx, e, "H2D");
+  st = cel_dev_extend_batch(ctx, nullptr, n, k, d_eds, d_rr, d_cr, d_dah, d_st, d_work, s, flags);
   if (st) return st;
   if (eds_out && (e = hipMemcpyAsync(eds_out, d_eds, eds_b, hipMemcpyDeviceToHost, s)) != hipSuccess)
     return hip_fail(ctx, e, "D2H");

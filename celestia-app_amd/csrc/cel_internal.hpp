@@ -43,6 +43,16 @@ struct RsGeom {
   uint32_t nsq;   // squares
 };
 
+// Several geometries of the same n in one launch (rs_axis.hip): tiles
+// [end[i-1], end[i]) belong to g[i].
+constexpr uint32_t kMaxSegs = 3;
+struct RsSegs {
+  RsGeom g[kMaxSegs];
+  uint32_t nslice[kMaxSegs];
+  uint32_t end[kMaxSegs];
+  uint32_t nseg;
+};
+
 constexpr uint32_t kTw16Words = 20;    // dwords of one GF(2^16) v_perm product table
 constexpr uint32_t kTw16Count = 4096;  // skew indices covered (2n - 1 < 4096 for n <= 2048)
 
@@ -62,6 +72,7 @@ void free_tables(DeviceTables* t);
 hipError_t launch_rs_encode(const RsGeom& g, const DeviceTables& t, hipStream_t s);
 hipError_t launch_rs_encode_bitslice(const RsGeom& g, hipStream_t s);  // GF(2^8), n <= 128
 hipError_t launch_rs_encode_axis(const RsGeom& g, hipStream_t s);       // GF(2^8), n <= 128
+hipError_t launch_rs_encode_axis_segs(const RsGeom* gs, uint32_t nseg, hipStream_t s);
 // Full 2D extension of nsq squares: Q0 rows -> Q1, then all 2k columns -> Q2|Q3.
 // ods == nullptr means Q0 is already in place inside eds.
 hipError_t launch_extend(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t nsq,

@@ -171,12 +171,25 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
 
 // DBG (profiling only, CEL_RS_DEBUG): 1 = loads and stores without the transform,
 // 2 = the transform without global memory traffic.
+//
+// One launch covers up to kMaxSegs geometries (RsSegs) of the same n: tiles
+// [end[i-1], end[i]) belong to segment i. The extension pipeline (launch_extend_axis)
+// puts the last column pass of chunk c-1 and both Q0 passes of chunk c in one launch.
 template <int LOGK, int DBG>
-__global__ __launch_bounds__(256, 3) void k_rs_axis_gf8(RsGeom g, uint32_t nslice, uint32_t ntiles) {
+__global__ __launch_bounds__(256, 3) void k_rs_axis_gf8(RsSegs sg) {
   constexpr int K = 1 << LOGK;
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t tile = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
-  if (tile >= ntiles) return;
+  uint32_t tile = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+  if (tile >= sg.end[sg.nseg - 1]) return;
+  uint32_t si = 0;
+#pragma unroll
+  for (uint32_t i = 0; i + 1 < kMaxSegs; i++) si += (tile >= sg.end[i] && i + 1 < sg.nseg) ? 1u : 0u;
+  si = __builtin_amdgcn_readfirstlane(si);
+  if (si > 0) tile -= sg.end[si - 1];
+  // field-wise selects on the scalar unit (a dynamic index into the kernarg struct
+  // would copy it to scratch)
+  const RsGeom g = si == 0 ? sg.g[0] : (si == 1 ? sg.g[1] : sg.g[2]);
+  const uint32_t nslice = si == 0 ? sg.nslice[0] : (si == 1 ? sg.nslice[1] : sg.nslice[2]);
   const uint32_t y = tile % nslice, r = tile / nslice;
   const uint32_t x = r % g.axes, z = r / g.axes;
   const uint32_t col = y * 256u + lane * 4u;
@@ -213,42 +226,61 @@ __global__ __launch_bounds__(256, 3) void k_rs_axis_gf8(RsGeom g, uint32_t nslic
 }
 
 template <int LOGK>
-hipError_t launch(const RsGeom& g, hipStream_t s, int dbg) {
-  const uint32_t nslice = (g.len + 255) / 256;
-  const uint64_t nt = (uint64_t)g.axes * nslice * g.nsq;
-  if (nt > 0xFFFFFFFFull) return hipErrorInvalidValue;
-  const uint32_t ntiles = (uint32_t)nt;
+hipError_t launch(const RsSegs& sg, hipStream_t s, int dbg) {
+  const uint32_t ntiles = sg.end[sg.nseg - 1];
+  if (ntiles == 0) return hipSuccess;
   const dim3 grid((ntiles + 3) / 4);
-  if (dbg == 1) hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 1>), grid, dim3(256), 0, s, g, nslice, ntiles);
-  else if (dbg == 2) hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 2>), grid, dim3(256), 0, s, g, nslice, ntiles);
-  else hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 0>), grid, dim3(256), 0, s, g, nslice, ntiles);
+  if (dbg == 1) hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 1>), grid, dim3(256), 0, s, sg);
+  else if (dbg == 2) hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 2>), grid, dim3(256), 0, s, sg);
+  else hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 0>), grid, dim3(256), 0, s, sg);
   return hipGetLastError();
 }
 
-
 }  // namespace ax
 
-// Byte offsets must fit the 32-bit buffer offsets: (n - 1) * shard stride + len < 2 GiB.
-hipError_t launch_rs_encode_axis(const RsGeom& g, hipStream_t s) {
+static int rs_debug() {
   static const int dbg = [] {
     const char* e = getenv("CEL_RS_DEBUG");
     return e ? atoi(e) : 0;
   }();
+  return dbg;
+}
+
+// Byte offsets must fit the 32-bit buffer offsets: (n - 1) * shard stride + len < 2 GiB.
+static bool geom_ok(const RsGeom& g) {
   const uint64_t span = (uint64_t)g.n * (g.in_shard > g.out_shard ? g.in_shard : g.out_shard) + g.len;
-  if (span >= 0x7fffffffull || (g.dcopy && (uint64_t)g.n * g.dc_shard + g.len >= 0x7fffffffull))
-    return hipErrorInvalidValue;
-  switch (g.n) {
-    case 1: return ax::launch<0>(g, s, dbg);
-    case 2: return ax::launch<1>(g, s, dbg);
-    case 4: return ax::launch<2>(g, s, dbg);
-    case 8: return ax::launch<3>(g, s, dbg);
-    case 16: return ax::launch<4>(g, s, dbg);
-    case 32: return ax::launch<5>(g, s, dbg);
-    case 64: return ax::launch<6>(g, s, dbg);
-    case 128: return ax::launch<7>(g, s, dbg);
+  return span < 0x7fffffffull && !(g.dcopy && (uint64_t)g.n * g.dc_shard + g.len >= 0x7fffffffull);
+}
+
+hipError_t launch_rs_encode_axis_segs(const RsGeom* gs, uint32_t nseg, hipStream_t s) {
+  if (nseg == 0 || nseg > kMaxSegs) return hipErrorInvalidValue;
+  RsSegs sg{};
+  uint64_t end = 0;
+  for (uint32_t i = 0; i < nseg; i++) {
+    const RsGeom& g = gs[i];
+    if (g.n != gs[0].n || !geom_ok(g) || g.len == 0) return hipErrorInvalidValue;
+    sg.g[i] = g;
+    sg.nslice[i] = (g.len + 255) / 256;
+    end += (uint64_t)g.axes * sg.nslice[i] * g.nsq;
+    if (end > 0xFFFFFFF0ull) return hipErrorInvalidValue;
+    sg.end[i] = (uint32_t)end;
+  }
+  sg.nseg = nseg;
+  const int dbg = rs_debug();
+  switch (gs[0].n) {
+    case 1: return ax::launch<0>(sg, s, dbg);
+    case 2: return ax::launch<1>(sg, s, dbg);
+    case 4: return ax::launch<2>(sg, s, dbg);
+    case 8: return ax::launch<3>(sg, s, dbg);
+    case 16: return ax::launch<4>(sg, s, dbg);
+    case 32: return ax::launch<5>(sg, s, dbg);
+    case 64: return ax::launch<6>(sg, s, dbg);
+    case 128: return ax::launch<7>(sg, s, dbg);
     default: return hipErrorInvalidValue;
   }
 }
+
+hipError_t launch_rs_encode_axis(const RsGeom& g, hipStream_t s) { return launch_rs_encode_axis_segs(&g, 1, s); }
 
 }  // namespace cel
 

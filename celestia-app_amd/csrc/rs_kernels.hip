@@ -745,37 +745,117 @@ hipError_t launch_rs_encode(const RsGeom& g, const DeviceTables& t, hipStream_t 
   return hipGetLastError();
 }
 
-hipError_t launch_extend(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t nsq, const DeviceTables& t,
-                         hipStream_t s) {
+// Squares per pipeline chunk of the wave-per-axis extension (CEL_RS_CHUNK, default 0 =
+// two launches over the whole batch: rows(Q0) -> Q1, then all 2k columns).
+// The chunked schedule (launch_extend_axis) re-reads Q0 and Q1 from the Infinity
+// Cache and cuts the memory-only time 9.57 -> 8.68 us per k=128 square, but with the
+// transform on it is slower (chunk 6: 14.9, chunk 8/12: 13.7 vs 12.3 us): the kernel
+// is VALU-bound and every small launch pays a full wave lifetime of tail
+// (profiles/r1_rs_chunk_ab.txt). Kept for A/B runs.
+static uint32_t rs_chunk(uint32_t) {
+  static const int env = [] {
+    const char* e = getenv("CEL_RS_CHUNK");
+    return e ? atoi(e) : 0;
+  }();
+  return env > 0 ? (uint32_t)env : 0u;
+}
+
+// Geometries of the extension of nsq squares starting at square `first`.
+//   rows(Q0) -> Q1, cols(Q0) -> Q2, cols(Q1) -> Q3
+// (Q2 = C*Q0 and Q3 = C*Q1 are exactly the reference's column pass over [Q0|Q1],
+// SURVEY A.4.) Q0 is read from `ods` (and copied into the EDS by the row pass) when
+// ods != nullptr, else from the EDS itself.
+struct ExtGeoms {
+  RsGeom rows, cols0, cols1;
+};
+static ExtGeoms ext_geoms(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t first, uint32_t nsq) {
   const uint64_t row = (uint64_t)2 * k * kShare;  // bytes per EDS row
   const uint64_t sq_eds = (uint64_t)4 * k * k * kShare;
   const uint64_t sq_ods = (uint64_t)k * k * kShare;
+  eds += first * sq_eds;
+  if (ods) ods += first * sq_ods;
+  ExtGeoms x{};
+  RsGeom& r = x.rows;
+  r.in = ods ? ods : eds;
+  r.in_sq = ods ? sq_ods : sq_eds;
+  r.in_axis = ods ? (uint64_t)k * kShare : row;
+  r.in_shard = kShare;
+  if (ods) {
+    r.dcopy = eds;
+    r.dc_sq = sq_eds;
+    r.dc_axis = row;
+    r.dc_shard = kShare;
+  }
+  r.out = eds + (uint64_t)k * kShare;
+  r.out_sq = sq_eds;
+  r.out_axis = row;
+  r.out_shard = kShare;
+  r.n = k;
+  r.len = kShare;
+  r.axes = k;
+  r.nsq = nsq;
+  RsGeom& c0 = x.cols0;
+  c0.in = ods ? ods : eds;
+  c0.in_sq = ods ? sq_ods : sq_eds;
+  c0.in_axis = kShare;
+  c0.in_shard = ods ? (uint64_t)k * kShare : row;
+  c0.out = eds + (uint64_t)k * row;
+  c0.out_sq = sq_eds;
+  c0.out_axis = kShare;
+  c0.out_shard = row;
+  c0.n = k;
+  c0.len = kShare;
+  c0.axes = k;
+  c0.nsq = nsq;
+  RsGeom& c1 = x.cols1;
+  c1 = c0;
+  c1.in = eds + (uint64_t)k * kShare;
+  c1.in_sq = sq_eds;
+  c1.in_shard = row;
+  c1.out = eds + (uint64_t)k * row + (uint64_t)k * kShare;
+  return x;
+}
+
+// Chunked schedule of the wave-per-axis kernel: launch j runs cols(Q1) of chunk j-1
+// beside rows(Q0) and cols(Q0) of chunk j. Every Q0 tile is read by a row tile and a
+// column tile of the same launch (the second read hits the Infinity Cache), and the
+// Q1 tiles that chunk j-1 wrote are re-read one launch later, still cache-resident.
+// The kernel boundary orders cols(Q1) after rows(Q0) of its chunk.
+static hipError_t launch_extend_axis(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t nsq, uint32_t chunk,
+                                     hipStream_t s) {
+  const uint32_t nch = (nsq + chunk - 1) / chunk;
+  for (uint32_t j = 0; j <= nch; j++) {
+    RsGeom gs[kMaxSegs];
+    uint32_t ns = 0;
+    if (j > 0) {
+      const uint32_t f = (j - 1) * chunk, n = (f + chunk <= nsq) ? chunk : nsq - f;
+      gs[ns++] = ext_geoms(ods, eds, k, f, n).cols1;
+    }
+    if (j < nch) {
+      const uint32_t f = j * chunk, n = (f + chunk <= nsq) ? chunk : nsq - f;
+      const ExtGeoms x = ext_geoms(ods, eds, k, f, n);
+      gs[ns++] = x.rows;
+      gs[ns++] = x.cols0;
+    }
+    const hipError_t e = launch_rs_encode_axis_segs(gs, ns, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+hipError_t launch_extend(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t nsq, const DeviceTables& t,
+                         hipStream_t s) {
+  if (nsq == 0) return hipSuccess;
+  if (k >= 32 && k <= 128 && use_axis_gf8(k)) {
+    const uint32_t chunk = rs_chunk(k);
+    if (chunk) return launch_extend_axis(ods, eds, k, nsq, chunk, s);
+  }
+  const uint64_t row = (uint64_t)2 * k * kShare;  // bytes per EDS row
+  const uint64_t sq_eds = (uint64_t)4 * k * k * kShare;
   hipError_t e;
   // Q0 rows -> Q1 (reading the ODS and writing Q0 into the EDS on the way when ods != nullptr)
-  RsGeom rows{};
-  if (ods) {
-    rows.in = ods;
-    rows.in_sq = sq_ods;
-    rows.in_axis = (uint64_t)k * kShare;
-    rows.dcopy = eds;
-    rows.dc_sq = sq_eds;
-    rows.dc_axis = row;
-    rows.dc_shard = kShare;
-  } else {
-    rows.in = eds;
-    rows.in_sq = sq_eds;
-    rows.in_axis = row;
-  }
-  rows.in_shard = kShare;
-  rows.out = eds + (uint64_t)k * kShare;
-  rows.out_sq = sq_eds;
-  rows.out_axis = row;
-  rows.out_shard = kShare;
-  rows.n = k;
-  rows.len = kShare;
-  rows.axes = k;
-  rows.nsq = nsq;
-  if ((e = launch_rs_encode(rows, t, s)) != hipSuccess) return e;
+  const ExtGeoms x = ext_geoms(ods, eds, k, 0, nsq);
+  if ((e = launch_rs_encode(x.rows, t, s)) != hipSuccess) return e;
   // columns of [Q0|Q1] -> [Q2|Q3]
   RsGeom cols{};
   cols.in = eds;

@@ -98,6 +98,15 @@ size_t cel_dev_workspace_size(uint32_t k, uint32_t n);
 cel_status cel_dev_extend_batch(cel_ctx* ctx, const void* d_ods, uint32_t n, uint32_t k,
                                 void* d_eds, void* d_row_roots, void* d_col_roots, void* d_dah,
                                 int32_t* d_status, void* d_work, void* stream, uint32_t flags);
+/* Input layout of the device path: d_ods == NULL means every ODS already sits in
+ * quadrant Q0 of its EDS buffer (row pitch 2k shares, the flattened rsmt2d square)
+ * and is extended in place. cel_dev_place_ods puts n
+ * row-major ODSs (host or device memory, as da.ExtendShares receives them flattened,
+ * data_availability_header.go:65-75) there with strided copies on `stream`.
+ * cel_extend_batch uses this path; a separate d_ods buffer makes the row pass also
+ * copy Q0 into the EDS. */
+cel_status cel_dev_place_ods(cel_ctx* ctx, const void* ods, uint32_t n, uint32_t k, void* d_eds,
+                             void* stream);
 /* Phase entry points of the same pipeline (for profiling and the row-sharded
  * multi-GPU mode): RS extension only, and NMT roots + DAH over a resident EDS. */
 cel_status cel_dev_extend_only(cel_ctx* ctx, const void* d_ods, uint32_t n, uint32_t k,

@@ -120,8 +120,9 @@ def test_gf16_square_k512(ctx, oracle):
 @pytest.mark.parametrize("k,n", [(32, 3), (64, 9), (64, 40), (128, 5), (128, 17)])
 def test_batch_extension_uneven(ctx, oracle, k, n):
     """Batches of the wave-per-axis kernel sizes (k = 32..128) with odd square counts:
-    (64, 40) and (128, 17) run the chunked row/column pipeline of launch_extend with a
-    short last chunk; EDS bytes, roots and DAH against the oracle for every square."""
+    (64, 40) and (128, 17) split into the two pipeline chunks of cel_dev_extend_batch
+    with a short last chunk; the host path places each ODS in Q0 and extends it in
+    place (cel_dev_place_ods). EDS bytes, roots and DAH against the oracle for every square."""
     import ctypes
     from celestia_eds import _lib
     odss = np.stack([random_ods(k, 900 + 7 * i + k) for i in range(n)])
@@ -190,3 +191,45 @@ def test_dah_validate_basic_cases(ctx):
                      (bad_hash, "wrong hash"), (mismatch, "unequal number of row and column roots")):
         with pytest.raises(CelError, match=msg):
             dah.ValidateBasic()
+
+
+@pytest.mark.parametrize("inplace", [True, False])
+@pytest.mark.parametrize("k,n", [(32, 5), (64, 3), (128, 13)])
+def test_device_batch(ctx, oracle, k, n, inplace):
+    """Device-resident batch (cel_dev_*). inplace: the ODS placed in Q0 of each EDS
+    buffer by cel_dev_place_ods and extended in place (d_ods = NULL, the bench's input
+    layout); otherwise a separate ODS buffer whose rows the row pass copies into Q0.
+    EDS bytes, roots and DAH against the oracle for every square; a second
+    extend_only over the same buffers is idempotent. (tools/gpu_pipe2.sh runs the
+    same test with CEL_RS_CHUNK=6: three chunks of the chunked schedule at (128, 13).)"""
+    import ctypes
+    from celestia_eds import _lib
+    from hipmem import DeviceBuffer, synchronize
+    odss = np.stack([random_ods(k, 4000 + 11 * i + k) for i in range(n)])
+    w = 2 * k
+    d_eds = DeviceBuffer(n * w * w * 512, fill=0xA5)  # Q1..Q3 must be fully overwritten
+    d_rr, d_cr = DeviceBuffer(n * w * 90), DeviceBuffer(n * w * 90)
+    d_dah, d_st = DeviceBuffer(n * 32), DeviceBuffer(n * 4, fill=0x7F)
+    d_work = DeviceBuffer(ctx.lib.cel_dev_workspace_size(k, n))
+    if inplace:
+        d_ods = None
+        ctx.check(ctx.lib.cel_dev_place_ods(ctx.handle, odss.ctypes.data_as(ctypes.c_void_p), n, k, d_eds.ptr, None))
+    else:
+        ods_buf = DeviceBuffer(odss.nbytes)
+        ods_buf.upload(odss)
+        d_ods = ods_buf.ptr
+    ctx.check(ctx.lib.cel_dev_extend_batch(ctx.handle, d_ods, n, k, d_eds.ptr, d_rr.ptr, d_cr.ptr, d_dah.ptr,
+                                           d_st.ptr, d_work.ptr,
+                                           None, _lib.FLAG_ORDER_CHECK))
+    synchronize()
+    eds = d_eds.download((n, w, w, 512))
+    rr, cr = d_rr.download((n, w, 90)), d_cr.download((n, w, 90))
+    dah, st = d_dah.download((n, 32)), d_st.download((n,), np.int32)
+    assert (st == 0).all()
+    for i in range(n):
+        e, r, c, d = oracle.extend_and_commit(odss[i])
+        assert np.array_equal(eds[i], e), f"square {i}: EDS differs"
+        assert np.array_equal(rr[i], r) and np.array_equal(cr[i], c) and dah[i].tobytes() == d
+    ctx.check(ctx.lib.cel_dev_extend_only(ctx.handle, d_ods, n, k, d_eds.ptr, None))
+    synchronize()
+    assert np.array_equal(d_eds.download((n, w, w, 512)), eds)

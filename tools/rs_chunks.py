@@ -16,6 +16,7 @@ ap.add_argument("--batch", type=int, default=32)
 ap.add_argument("--chunks", type=int, nargs="+", default=[1, 2, 4, 8, 32])
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--streams", type=int, default=1)
+ap.add_argument("--inplace", action="store_true", help="Q0 already in the EDS (d_ods = NULL)")
 a = ap.parse_args()
 from celestia_eds.device import SquareBatch  # noqa: E402
 from celestia_eds.testfactory import random_ods  # noqa: E402
@@ -39,7 +40,7 @@ def run(cs):
     for i, s0 in enumerate(range(0, B, cs)):
         n = min(cs, B - s0)
         st = streams[i % len(streams)] if a.streams > 1 else sb.hip_stream
-        c.check(c.lib.cel_dev_extend_only(c.handle, ctypes.c_void_p(sb.ods.data_ptr() + s0 * ods_sq), n, k,
+        c.check(c.lib.cel_dev_extend_only(c.handle, None if a.inplace else ctypes.c_void_p(sb.ods.data_ptr() + s0 * ods_sq), n, k,
                                           ctypes.c_void_p(sb.eds.data_ptr() + s0 * eds_sq),
                                           ctypes.c_void_p(st.cuda_stream)))
     for st in streams:
@@ -57,7 +58,7 @@ for cs in a.chunks:
     e1.record(sb.hip_stream)
     e1.synchronize()
     us = e0.elapsed_time(e1) / a.reps * 1e3 / B
-    print(f"{os.environ.get('CEL_RS_IMPL', 'default'):9s} dbg={os.environ.get('CEL_RS_DEBUG', '0')} streams={a.streams} k={k} chunk={cs:3d}: {us:6.2f} us/square "
+    print(f"{os.environ.get('CEL_RS_IMPL', 'default'):9s} dbg={os.environ.get('CEL_RS_DEBUG', '0')} inplace={int(a.inplace)} streams={a.streams} k={k} chunk={cs:3d}: {us:6.2f} us/square "
           f"= {2048 * k * k / us / 1e3:7.1f} GB/s algorithmic ({2048 * k * k / us / 1e3 / 8000 * 100:4.1f} %)")
 
 if os.environ.get("CEL_COPY_REF"):
