@@ -14,6 +14,7 @@
 // CEL_EDEVICE.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <climits>
 #include <cstdlib>
 #include <cmath>
@@ -728,121 +729,84 @@ struct RepairBufs {
   uint8_t* dmask;
   uint8_t* tmp;
   int32_t* idx;
-  int32_t* flags;
-  uint32_t* roots;
-  void* work;
+  int32_t* flags;  // [2][W] encoding-check flags by (direction, axis)
 };
 
-// Verify (and for solve=true, decode first) a list of axes. Returns CEL_OK, or
-// CEL_EBYZANTINE with *bad set to the list entry that failed.
-cel_status process_axes(cel_ctx* ctx, const RepairBufs& b, uint32_t k, int is_col, const std::vector<int32_t>& list,
-                        const uint8_t* exp_roots, bool solve, int32_t* bad) {
+// One crossword pass over `list` (axes of one direction with >= k known cells):
+// decode them, re-encode the data half and compare it with the decoded parity half
+// (rsmt2d verifyEncoding); mismatches set flags_all[is_col*W + axis]. Nothing is
+// synchronised: every check result is read back once at the end of the repair.
+static cel_status solve_pass(cel_ctx* ctx, const RepairBufs& b, uint32_t k, int is_col,
+                             const std::vector<int32_t>& list) {
   const uint32_t W = 2 * k, na = (uint32_t)list.size();
   hipStream_t s = ctx->stream;
   hipError_t e;
-  if ((e = hipMemcpyAsync(b.idx, list.data(), na * 4, hipMemcpyHostToDevice, s)) != hipSuccess) return hip_fail(ctx, e, "H2D");
-  if ((e = hipMemsetAsync(b.flags, 0, na * 4, s)) != hipSuccess) return hip_fail(ctx, e, "memset");
+  if ((e = hipMemcpyAsync(b.idx, list.data(), na * 4, hipMemcpyHostToDevice, s)) != hipSuccess)
+    return hip_fail(ctx, e, "H2D");
   if ((e = launch_gather_axes(b.eds, b.mask, W, b.idx, is_col, na, b.dense, b.dmask, s)) != hipSuccess)
     return hip_fail(ctx, e, "gather");
-  if (solve) {
-    if ((e = launch_rs_decode(b.dense, b.dmask, na, k, kShare, ctx->tables, nullptr, s)) != hipSuccess)
-      return hip_fail(ctx, e, "decode");
-    // re-encode the data half and compare with the parity half (rsmt2d verifyEncoding)
-    RsGeom g{};
-    g.in = b.dense;
-    g.in_sq = (uint64_t)na * W * kShare;
-    g.in_axis = (uint64_t)W * kShare;
-    g.in_shard = kShare;
-    g.out = b.tmp;
-    g.out_sq = (uint64_t)na * k * kShare;
-    g.out_axis = (uint64_t)k * kShare;
-    g.out_shard = kShare;
-    g.n = k;
-    g.len = kShare;
-    g.axes = na;
-    g.nsq = 1;
-    if ((e = launch_rs_encode(g, ctx->tables, s)) != hipSuccess) return hip_fail(ctx, e, "re-encode");
-    if ((e = launch_cmp(b.tmp, (uint64_t)k * kShare, b.dense + (uint64_t)k * kShare, (uint64_t)W * kShare,
-                        (uint64_t)k * kShare, na, b.flags, s)) != hipSuccess)
-      return hip_fail(ctx, e, "compare");
-  }
-  if ((e = launch_axes_roots(b.dense, k, b.idx, na, b.roots, b.work, s)) != hipSuccess) return hip_fail(ctx, e, "roots");
-  std::vector<int32_t> flags(na);
-  std::vector<uint32_t> roots((size_t)na * kNodeWords);
-  if ((e = hipMemcpyAsync(flags.data(), b.flags, na * 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
-      (e = hipMemcpyAsync(roots.data(), b.roots, roots.size() * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
-    return hip_fail(ctx, e, "D2H");
-  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "sync");
-  for (uint32_t a = 0; a < na; a++) {
-    const uint8_t* got = reinterpret_cast<const uint8_t*>(&roots[(size_t)a * kNodeWords]);
-    if (flags[a] || std::memcmp(got, exp_roots + (size_t)list[a] * kNode, kNode) != 0) {
-      *bad = list[a];
-      return CEL_EBYZANTINE;
-    }
-  }
-  if (solve && (e = launch_scatter_axes(b.eds, b.mask, W, b.idx, is_col, na, b.dense, s)) != hipSuccess)
+  if ((e = launch_rs_decode(b.dense, b.dmask, na, k, kShare, ctx->tables, nullptr, s)) != hipSuccess)
+    return hip_fail(ctx, e, "decode");
+  RsGeom g{};
+  g.in = b.dense;
+  g.in_sq = (uint64_t)na * W * kShare;
+  g.in_axis = (uint64_t)W * kShare;
+  g.in_shard = kShare;
+  g.out = b.tmp;
+  g.out_sq = (uint64_t)na * k * kShare;
+  g.out_axis = (uint64_t)k * kShare;
+  g.out_shard = kShare;
+  g.n = k;
+  g.len = kShare;
+  g.axes = na;
+  g.nsq = 1;
+  if ((e = launch_rs_encode(g, ctx->tables, s)) != hipSuccess) return hip_fail(ctx, e, "re-encode");
+  if ((e = launch_cmp(b.tmp, (uint64_t)k * kShare, b.dense + (uint64_t)k * kShare, (uint64_t)W * kShare,
+                      (uint64_t)k * kShare, na, b.flags + (size_t)is_col * W, s, b.idx)) != hipSuccess)
+    return hip_fail(ctx, e, "compare");
+  if ((e = launch_scatter_axes(b.eds, b.mask, W, b.idx, is_col, na, b.dense, s)) != hipSuccess)
     return hip_fail(ctx, e, "scatter");
+  // the next pass rewrites b.idx: the stream orders it after this pass's kernels, and
+  // the host list is read before hipMemcpyAsync returns (pageable source)
   return CEL_OK;
 }
 
-}  // namespace
-
-cel_status cel_repair(cel_ctx* ctx, uint8_t* eds, uint8_t* present, uint32_t k, uint32_t share_size,
-                      const uint8_t* row_roots, const uint8_t* col_roots, int32_t* bad_axis, int32_t* bad_index) {
-  if (!ctx) return CEL_EINVAL;
-  std::lock_guard<std::mutex> lock(ctx->mu);
-  if (!eds || !present || !row_roots || !col_roots) return fail(ctx, CEL_EINVAL, "nil argument");
-  cel_status st = validate_square(ctx, k, share_size);
-  if (st) return st;
-  if (k > 512) return fail(ctx, CEL_ETOOBIG, "square too wide for the device decoder");
-  if (bad_axis) *bad_axis = -1;
-  if (bad_index) *bad_index = -1;
-  DeviceGuard g(ctx->device);
+// rsmt2d Repair over the EDS resident at b.eds. hm = host presence mask (updated).
+// The crossword control loop runs on the host over the mask; no pass waits for the
+// device. Root checks are deferred: an axis, once complete, never changes, so one
+// commit pass over the final square gives every root rsmt2d checks along the way, and
+// the checks are replayed in rsmt2d's order (prerepairSanityCheck rows then columns,
+// then each solved axis in pass order, encoding check before root check, then the
+// final all-axes verification), reporting the same first failing axis.
+static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>& hm, uint32_t k,
+                              const uint8_t* row_roots, const uint8_t* col_roots, int32_t* bad_axis,
+                              int32_t* bad_index) {
   const uint32_t W = 2 * k;
-  const size_t cells = (size_t)W * W, eds_b = cells * kShare;
-  hipError_t e = hipSuccess;
-  RepairBufs b{};
-  b.eds = static_cast<uint8_t*>(scratch(ctx, S_EDS, eds_b, &e));
-  b.dense = static_cast<uint8_t*>(scratch(ctx, S_IN, eds_b, &e));
-  b.tmp = static_cast<uint8_t*>(scratch(ctx, S_AUX, eds_b / 2 + cells + 3 * (size_t)W * 4 + 256, &e));
-  b.work = scratch(ctx, S_WORK, axes_roots_workspace_size(k, W), &e);
-  b.roots = static_cast<uint32_t*>(scratch(ctx, S_ROOTS, (size_t)W * kNodeWords * 4 + 4 * kNodeWords * 4 * W, &e));
-  b.mask = static_cast<uint8_t*>(scratch(ctx, S_MASK, 2 * cells + 256, &e));
-  if (!b.eds || !b.dense || !b.tmp || !b.work || !b.roots || !b.mask)
-    return fail(ctx, CEL_ENOMEM, "device allocation failed");
-  b.dmask = b.mask + ((cells + 255) & ~(size_t)255);
-  uint8_t* aux = b.tmp + eds_b / 2;
-  b.idx = reinterpret_cast<int32_t*>(aux);
-  b.flags = reinterpret_cast<int32_t*>(aux + (size_t)W * 4);
+  const size_t cells = (size_t)W * W;
   hipStream_t s = ctx->stream;
-  std::vector<uint8_t> hm(cells);
-  for (size_t i = 0; i < cells; i++) hm[i] = present[i] ? 1 : 0;
-  if ((e = hipMemcpyAsync(b.eds, eds, eds_b, hipMemcpyHostToDevice, s)) != hipSuccess ||
-      (e = hipMemcpyAsync(b.mask, hm.data(), cells, hipMemcpyHostToDevice, s)) != hipSuccess)
+  hipError_t e = hipSuccess;
+  cel_status st;
+  if ((e = hipMemcpyAsync(b.mask, hm.data(), cells, hipMemcpyHostToDevice, s)) != hipSuccess ||
+      (e = hipMemsetAsync(b.flags, 0, 2 * (size_t)W * 4, s)) != hipSuccess)
     return hip_fail(ctx, e, "H2D");
   auto count = [&](int is_col, uint32_t i) {
     uint32_t c = 0;
     for (uint32_t j = 0; j < W; j++) c += is_col ? hm[(size_t)j * W + i] : hm[(size_t)i * W + j];
     return c;
   };
-  auto byz = [&](int is_col, int32_t idx) {
-    if (bad_axis) *bad_axis = is_col;
-    if (bad_index) *bad_index = idx;
-    return fail(ctx, CEL_EBYZANTINE, std::string("byzantine ") + (is_col ? "column" : "row") + " " +
-                                         std::to_string(idx));
+  struct Check {
+    int is_col;
+    int32_t idx;
+    bool solved;  // also has an encoding-check flag
   };
+  std::vector<Check> order;
   // prerepairSanityCheck: complete axes must match their roots.
-  for (int is_col = 0; is_col < 2; is_col++) {
-    std::vector<int32_t> list;
+  for (int is_col = 0; is_col < 2; is_col++)
     for (uint32_t i = 0; i < W; i++)
-      if (count(is_col, i) == W) list.push_back((int32_t)i);
-    if (list.empty()) continue;
-    int32_t bad = -1;
-    st = process_axes(ctx, b, k, is_col, list, is_col ? col_roots : row_roots, false, &bad);
-    if (st == CEL_EBYZANTINE) return byz(is_col, bad);
-    if (st) return st;
-  }
+      if (count(is_col, i) == W) order.push_back({is_col, (int32_t)i, false});
   // crossword: alternate rows and columns until solved or stuck
+  std::vector<std::vector<int32_t>> lists;  // kept alive until the final sync
+  bool solved = false;
   for (;;) {
     bool progress = false;
     for (int is_col = 0; is_col < 2; is_col++) {
@@ -852,33 +816,122 @@ cel_status cel_repair(cel_ctx* ctx, uint8_t* eds, uint8_t* present, uint32_t k, 
         if (c >= k && c < W) list.push_back((int32_t)i);
       }
       if (list.empty()) continue;
-      int32_t bad = -1;
-      st = process_axes(ctx, b, k, is_col, list, is_col ? col_roots : row_roots, true, &bad);
-      if (st == CEL_EBYZANTINE) return byz(is_col, bad);
-      if (st) return st;
-      for (int32_t i : list)
+      if ((st = solve_pass(ctx, b, k, is_col, list)) != CEL_OK) return st;
+      for (int32_t i : list) {
+        order.push_back({is_col, i, true});
         for (uint32_t j = 0; j < W; j++) {
           if (is_col) hm[(size_t)j * W + i] = 1;
           else hm[(size_t)i * W + j] = 1;
         }
+      }
+      lists.push_back(std::move(list));
       progress = true;
     }
     size_t have = 0;
     for (size_t i = 0; i < cells; i++) have += hm[i];
-    if (have == cells) break;
-    if (!progress) return fail(ctx, CEL_EUNREPAIRABLE, "failed to solve data square");
+    if (have == cells) {
+      solved = true;
+      break;
+    }
+    if (!progress) break;
   }
+  // every root of the (possibly partial) square in one commit pass, roots only
+  const size_t roots_b = (size_t)W * kNode;
+  uint8_t* d_rr = b.tmp;  // free after the last solve pass (stream order)
+  uint8_t* d_cr = b.tmp + roots_b;
+  if ((e = launch_commit(b.eds, k, 1, d_rr, d_cr, nullptr, nullptr, b.dense, false, s)) != hipSuccess)
+    return hip_fail(ctx, e, "roots");
+  std::vector<uint8_t> got(2 * roots_b);
+  std::vector<int32_t> flags(2 * (size_t)W);
+  if ((e = hipMemcpyAsync(got.data(), d_rr, 2 * roots_b, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+      (e = hipMemcpyAsync(flags.data(), b.flags, flags.size() * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+    return hip_fail(ctx, e, "D2H");
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "sync");
+  auto root_ok = [&](int is_col, int32_t i) {
+    const uint8_t* exp = (is_col ? col_roots : row_roots) + (size_t)i * kNode;
+    return std::memcmp(got.data() + is_col * roots_b + (size_t)i * kNode, exp, kNode) == 0;
+  };
+  auto byz = [&](int is_col, int32_t idx) {
+    if (bad_axis) *bad_axis = is_col;
+    if (bad_index) *bad_index = idx;
+    return fail(ctx, CEL_EBYZANTINE, std::string("byzantine ") + (is_col ? "column" : "row") + " " +
+                                         std::to_string(idx));
+  };
+  for (const Check& c : order)
+    if ((c.solved && flags[(size_t)c.is_col * W + c.idx]) || !root_ok(c.is_col, c.idx)) return byz(c.is_col, c.idx);
+  if (!solved) return fail(ctx, CEL_EUNREPAIRABLE, "failed to solve data square");
   // Every axis solved along one direction must also match on the other.
-  for (int is_col = 0; is_col < 2; is_col++) {
-    std::vector<int32_t> list(W);
-    for (uint32_t i = 0; i < W; i++) list[i] = (int32_t)i;
-    int32_t bad = -1;
-    st = process_axes(ctx, b, k, is_col, list, is_col ? col_roots : row_roots, false, &bad);
-    if (st == CEL_EBYZANTINE) return byz(is_col, bad);
-    if (st) return st;
-  }
+  for (int is_col = 0; is_col < 2; is_col++)
+    for (uint32_t i = 0; i < W; i++)
+      if (!root_ok(is_col, (int32_t)i)) return byz(is_col, (int32_t)i);
+  return CEL_OK;
+}
+
+static cel_status repair_bufs(cel_ctx* ctx, uint32_t k, bool own_eds, RepairBufs* b) {
+  const uint32_t W = 2 * k;
+  const size_t cells = (size_t)W * W, eds_b = cells * kShare;
+  hipError_t e = hipSuccess;
+  if (own_eds) b->eds = static_cast<uint8_t*>(scratch(ctx, S_EDS, eds_b, &e));
+  // dense doubles as the commit workspace of the final verification
+  const size_t dense_b = std::max(eds_b, nmt_workspace_size(k, 1));
+  b->dense = static_cast<uint8_t*>(scratch(ctx, S_IN, dense_b, &e));
+  b->tmp = static_cast<uint8_t*>(scratch(ctx, S_AUX, eds_b / 2 + cells + 3 * (size_t)W * 4 + 256, &e));
+  b->mask = static_cast<uint8_t*>(scratch(ctx, S_MASK, 2 * cells + 256, &e));
+  if (!b->eds || !b->dense || !b->tmp || !b->mask)
+    return fail(ctx, CEL_ENOMEM, "device allocation failed");
+  b->dmask = b->mask + ((cells + 255) & ~(size_t)255);
+  uint8_t* aux = b->tmp + eds_b / 2;
+  b->idx = reinterpret_cast<int32_t*>(aux);
+  b->flags = reinterpret_cast<int32_t*>(aux + (size_t)W * 4);
+  return CEL_OK;
+}
+
+}  // namespace
+
+
+cel_status cel_repair(cel_ctx* ctx, uint8_t* eds, uint8_t* present, uint32_t k, uint32_t share_size,
+                      const uint8_t* row_roots, const uint8_t* col_roots, int32_t* bad_axis, int32_t* bad_index) {
+  if (!ctx) return CEL_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (!eds || !present || !row_roots || !col_roots) return fail(ctx, CEL_EINVAL, "nil argument");
+  cel_status st = validate_square(ctx, k, share_size);
+  if (st) return st;
+  if (bad_axis) *bad_axis = -1;
+  if (bad_index) *bad_index = -1;
+  DeviceGuard g(ctx->device);
+  const uint32_t W = 2 * k;
+  const size_t cells = (size_t)W * W, eds_b = cells * kShare;
+  RepairBufs b{};
+  if ((st = repair_bufs(ctx, k, true, &b)) != CEL_OK) return st;
+  hipStream_t s = ctx->stream;
+  hipError_t e;
+  std::vector<uint8_t> hm(cells);
+  for (size_t i = 0; i < cells; i++) hm[i] = present[i] ? 1 : 0;
+  if ((e = hipMemcpyAsync(b.eds, eds, eds_b, hipMemcpyHostToDevice, s)) != hipSuccess) return hip_fail(ctx, e, "H2D");
+  if ((st = repair_core(ctx, b, hm, k, row_roots, col_roots, bad_axis, bad_index)) != CEL_OK) return st;
   if ((e = hipMemcpyAsync(eds, b.eds, eds_b, hipMemcpyDeviceToHost, s)) != hipSuccess) return hip_fail(ctx, e, "D2H");
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "sync");
+  for (size_t i = 0; i < cells; i++) present[i] = 1;
+  return CEL_OK;
+}
+
+cel_status cel_dev_repair(cel_ctx* ctx, void* d_eds, uint8_t* present, uint32_t k, const uint8_t* row_roots,
+                          const uint8_t* col_roots, int32_t* bad_axis, int32_t* bad_index) {
+  if (!ctx) return CEL_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (!d_eds || !present || !row_roots || !col_roots) return fail(ctx, CEL_EINVAL, "nil argument");
+  cel_status st = validate_square(ctx, k, kShare);
+  if (st) return st;
+  if (bad_axis) *bad_axis = -1;
+  if (bad_index) *bad_index = -1;
+  DeviceGuard g(ctx->device);
+  const size_t cells = (size_t)4 * k * k;
+  RepairBufs b{};
+  b.eds = static_cast<uint8_t*>(d_eds);
+  if ((st = repair_bufs(ctx, k, false, &b)) != CEL_OK) return st;
+  std::vector<uint8_t> hm(cells);
+  for (size_t i = 0; i < cells; i++) hm[i] = present[i] ? 1 : 0;
+  if ((st = repair_core(ctx, b, hm, k, row_roots, col_roots, bad_axis, bad_index)) != CEL_OK) return st;
   for (size_t i = 0; i < cells; i++) present[i] = 1;
   return CEL_OK;
 }

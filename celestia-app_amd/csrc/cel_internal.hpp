@@ -110,7 +110,7 @@ hipError_t launch_gather_axes(const uint8_t* eds, const uint8_t* mask, uint32_t 
 hipError_t launch_scatter_axes(uint8_t* eds, uint8_t* mask, uint32_t W, const int32_t* idx, int is_col,
                                uint32_t naxes, const uint8_t* dense, hipStream_t s);
 hipError_t launch_cmp(const uint8_t* x, uint64_t xstride, const uint8_t* y, uint64_t ystride, uint64_t bytes,
-                      uint32_t naxes, int32_t* flags, hipStream_t s);
+                      uint32_t naxes, int32_t* flags, hipStream_t s, const int32_t* idx = nullptr);
 size_t axes_roots_workspace_size(uint32_t k, uint32_t naxes);
 hipError_t launch_axes_roots(const uint8_t* cells, uint32_t k, const int32_t* axis_idx, uint32_t naxes,
                              uint32_t* roots, void* work, hipStream_t s);

@@ -251,11 +251,10 @@ __device__ __forceinline__ void hash_node(const uint32_t (&L)[kNodeWords], const
 //   otherwise  : in[sq][t][2j], in[sq][t][2j+1] with `nin` nodes per tree.
 __device__ __forceinline__ void rfc_leaf90(const uint32_t (&R)[kNodeWords], uint32_t (&st)[8]);
 
-// One tree level for all trees. With LEAFD != nullptr this is the root level: each lane
-// also hashes its root as an RFC-6962 leaf of the DAH tree (2 compressions) so the
-// per-square DAH kernel starts from leaf digests.
-// At the root level (leafd != nullptr) the lane also writes its root, packed to 90
-// bytes, straight into the caller's row_out / col_out ([nsq][W][90]).
+// One tree level for all trees. At the root level the lane writes its root, packed to
+// 90 bytes, straight into the caller's row_out / col_out ([nsq][W][90]); with
+// leafd != nullptr it also hashes the root as an RFC-6962 leaf of the DAH tree
+// (2 compressions) so the per-square DAH kernel starts from leaf digests.
 template <bool FROM_LEAVES>
 __global__ CEL_LEVEL_BOUNDS void k_level(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint32_t W,
                                                uint32_t nin, uint32_t trees, uint32_t* __restrict__ leafd,
@@ -280,14 +279,16 @@ __global__ CEL_LEVEL_BOUNDS void k_level(const uint32_t* __restrict__ in, uint32
   hash_node(L, R, o);
   const uint64_t oi = (uint64_t)blockIdx.y * trees * nout + idx;
   store_node(out + oi * kNodeWords, o);
-  if (leafd) {
-    if (row_out) {  // 90-byte record at a 2-byte aligned address: 45 halfword stores
+  if (row_out) {
+    {  // 90-byte record at a 2-byte aligned address: 45 halfword stores
       uint8_t* r = (t < W ? row_out + ((uint64_t)blockIdx.y * W + t) * kNode
                           : col_out + ((uint64_t)blockIdx.y * W + (t - W)) * kNode);
       uint16_t* r16 = reinterpret_cast<uint16_t*>(r);
 #pragma unroll
       for (int i = 0; i < 45; i++) r16[i] = (uint16_t)(o[i / 2] >> (16 * (i & 1)));
     }
+  }
+  if (leafd) {
     uint32_t st[8];
     rfc_leaf90(o, st);
     uint4* d = reinterpret_cast<uint4*>(leafd + oi * 8);
@@ -464,7 +465,7 @@ hipError_t launch_commit(const uint8_t* eds, uint32_t k, uint32_t nsq, uint8_t* 
   while (nin > 1) {
     const uint32_t nout = nin / 2;
     uint32_t* out = (nout == 1) ? roots : dst;
-    uint32_t* ld = (nout == 1) ? leafd : nullptr;
+    uint32_t* ld = (nout == 1 && dah) ? leafd : nullptr;  // dah == nullptr: roots only
     dim3 g((trees * nout + 255) / 256, nsq);
     uint8_t* ro = (nout == 1) ? row_roots : nullptr;
     uint8_t* co = (nout == 1) ? col_roots : nullptr;
@@ -477,7 +478,8 @@ hipError_t launch_commit(const uint8_t* eds, uint32_t k, uint32_t nsq, uint8_t* 
   }
   const size_t lds = (size_t)trees * 8 * 4;
   // roots already packed into row_roots / col_roots by the root level
-  hipLaunchKernelGGL(k_merkle, dim3(nsq), dim3(256), lds, s, roots, leafd, trees, dah, nullptr, nullptr, bad, status);
+  if (dah)
+    hipLaunchKernelGGL(k_merkle, dim3(nsq), dim3(256), lds, s, roots, leafd, trees, dah, nullptr, nullptr, bad, status);
   return hipGetLastError();
 }
 

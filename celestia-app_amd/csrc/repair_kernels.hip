@@ -43,7 +43,8 @@ __global__ __launch_bounds__(256) void k_scatter_axes(uint8_t* __restrict__ eds,
 // flags[a] |= 1 if the n bytes of a[axis] and b[axis] differ (uint4 granularity).
 __global__ __launch_bounds__(256) void k_cmp(const uint8_t* __restrict__ x, uint64_t xstride,
                                              const uint8_t* __restrict__ y, uint64_t ystride, uint64_t bytes,
-                                             uint32_t naxes, int32_t* __restrict__ flags) {
+                                             uint32_t naxes, int32_t* __restrict__ flags,
+                                             const int32_t* __restrict__ idx) {
   const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
   const uint64_t per = bytes / 16;
   if (t >= per * naxes) return;
@@ -51,7 +52,7 @@ __global__ __launch_bounds__(256) void k_cmp(const uint8_t* __restrict__ x, uint
   const uint64_t q = t % per;
   const uint4 u = reinterpret_cast<const uint4*>(x + a * xstride)[q];
   const uint4 v = reinterpret_cast<const uint4*>(y + a * ystride)[q];
-  if (u.x != v.x || u.y != v.y || u.z != v.z || u.w != v.w) atomicOr(flags + a, 1);
+  if (u.x != v.x || u.y != v.y || u.z != v.z || u.w != v.w) atomicOr(flags + (idx ? idx[a] : (int32_t)a), 1);
 }
 
 hipError_t launch_gather_axes(const uint8_t* eds, const uint8_t* mask, uint32_t W, const int32_t* idx, int is_col,
@@ -71,10 +72,10 @@ hipError_t launch_scatter_axes(uint8_t* eds, uint8_t* mask, uint32_t W, const in
 }
 
 hipError_t launch_cmp(const uint8_t* x, uint64_t xstride, const uint8_t* y, uint64_t ystride, uint64_t bytes,
-                      uint32_t naxes, int32_t* flags, hipStream_t s) {
+                      uint32_t naxes, int32_t* flags, hipStream_t s, const int32_t* idx) {
   const uint64_t total = (bytes / 16) * naxes;
   hipLaunchKernelGGL(k_cmp, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, x, xstride, y, ystride, bytes,
-                     naxes, flags);
+                     naxes, flags, idx);
   return hipGetLastError();
 }
 

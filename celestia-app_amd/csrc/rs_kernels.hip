@@ -930,40 +930,142 @@ __device__ void decode_chunk(const Ops& ops, uint32_t* lds, uint32_t* err, const
   __syncthreads();
 }
 
+// GF(2^8) decode of one 64-byte chunk with v_perm product tables staged in LDS
+// (ltw: twiddle tables by skew index, lmul: tables by log value; 5 dwords each) in
+// place of the per-byte log/exp lookups of Gf8Ops: same transform as decode_chunk,
+// with shift-only butterfly indexing.
+__device__ void decode_chunk_gf8p(uint32_t* lds, const uint32_t* err, const uint8_t* pres, uint32_t m,
+                                  const uint32_t* ltw, const uint32_t* lmul) {
+  const uint32_t n = 2 * m;
+  const uint32_t lgn = 31u - __builtin_clz(n);
+  constexpr uint32_t U = 16;  // dwords per 64-byte chunk
+  auto tab = [](const uint32_t* t) { return PermTab{t[0], t[1], t[2], t[3], t[4]}; };
+  for (uint32_t it = threadIdx.x; it < n * U; it += blockDim.x) {
+    const uint32_t i = it / U, u = it % U;
+    if (pres[i]) lds[i * 16 + u] = gf8_mul4(lds[i * 16 + u], tab(lmul + err[i] * 5));
+  }
+  __syncthreads();
+  const uint32_t items = (n / 2) * U;
+  for (uint32_t lD = 0; lD < lgn; lD++) {  // IFFT, offset 0
+    const uint32_t D = 1u << lD;
+    for (uint32_t it = threadIdx.x; it < items; it += blockDim.x) {
+      const uint32_t pair = it / U, u = it % U;
+      const uint32_t base = (pair >> lD) << (lD + 1), a = base + (pair & (D - 1));
+      uint32_t* x = lds + a * 16 + u;
+      uint32_t* y = lds + (a + D) * 16 + u;
+      const uint32_t idx = base + D - 1;
+      const uint32_t yv = *y ^ *x;
+      *y = yv;
+      if (c_gf8.skew[idx] != 255u) *x ^= gf8_mul4(yv, tab(ltw + idx * 5));
+    }
+    __syncthreads();
+  }
+  // formal derivative (see decode_chunk)
+  for (uint32_t base = 0; base < n * U; base += blockDim.x) {
+    const uint32_t it = base + threadIdx.x;
+    uint32_t acc = 0;
+    const bool active = it < n * U;
+    uint32_t x = 0, u = 0;
+    if (active) {
+      x = it / U;
+      u = it % U;
+      for (uint32_t t = 1; t < n; t <<= 1)
+        if ((x & t) == 0 && x + t < n) acc ^= lds[(x + t) * 16 + u];
+    }
+    __syncthreads();
+    if (active) lds[x * 16 + u] ^= acc;
+    __syncthreads();
+  }
+  for (uint32_t lD = lgn; lD-- > 0;) {  // FFT
+    const uint32_t D = 1u << lD;
+    for (uint32_t it = threadIdx.x; it < items; it += blockDim.x) {
+      const uint32_t pair = it / U, u = it % U;
+      const uint32_t base = (pair >> lD) << (lD + 1), a = base + (pair & (D - 1));
+      uint32_t* x = lds + a * 16 + u;
+      uint32_t* y = lds + (a + D) * 16 + u;
+      const uint32_t idx = base + D - 1;
+      uint32_t xv = *x;
+      if (c_gf8.skew[idx] != 255u) xv ^= gf8_mul4(*y, tab(ltw + idx * 5));
+      *x = xv;
+      *y ^= xv;
+    }
+    __syncthreads();
+  }
+  for (uint32_t it = threadIdx.x; it < n * U; it += blockDim.x) {
+    const uint32_t i = it / U, u = it % U;
+    if (!pres[i]) lds[i * 16 + u] = gf8_mul4(lds[i * 16 + u], tab(lmul + ((255u - err[i]) % 255u) * 5));
+  }
+  __syncthreads();
+}
+
 // grid: x = axis, y = 64-byte chunk. shards: [naxes][2m][len] in rsmt2d order
 // (data then parity); present: [naxes][2m].
 template <bool GF16>
 __global__ __launch_bounds__(256) void k_rs_decode(uint8_t* shards, const uint8_t* present, uint32_t m,
                                                    uint32_t len, const uint16_t* __restrict__ gexp,
                                                    const uint16_t* __restrict__ glog,
-                                                   const uint16_t* __restrict__ gskew) {
+                                                   const uint16_t* __restrict__ gskew,
+                                                   const uint32_t* __restrict__ tw8,
+                                                   const uint32_t* __restrict__ mul8) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const uint32_t n = 2 * m;
   uint32_t* err = lds + n * 16;
-  uint8_t* pres = reinterpret_cast<uint8_t*>(err + n);
-  __shared__ uint8_t s_exp[256], s_log[256];
+  uint32_t* ltw = err + 2 * n;      // (err + n: n words of error-locator scratch)
+  uint32_t* lmul = ltw + 255 * 5;   // GF(2^8): [255][5] twiddle tables, [256][5] by log value
+  uint8_t* pres = reinterpret_cast<uint8_t*>(GF16 ? ltw : lmul + 256 * 5);
+  if (!GF16) {
+    for (uint32_t i = threadIdx.x; i < 255 * 5; i += blockDim.x) ltw[i] = tw8[(i / 5) * 8 + i % 5];
+    for (uint32_t i = threadIdx.x; i < 256 * 5; i += blockDim.x) lmul[i] = mul8[(i / 5) * 8 + i % 5];
+  }
+  __shared__ uint8_t s_log[256];
   uint8_t* axis = shards + (uint64_t)blockIdx.x * n * len;
   const uint8_t* pa = present + (uint64_t)blockIdx.x * n;
   // position p in Leopard order: p < m -> parity shard p (rsmt2d index m + p); else data p - m.
   for (uint32_t p = threadIdx.x; p < n; p += blockDim.x) pres[p] = pa[p < m ? m + p : p - m] ? 1 : 0;
   if (!GF16) {
     for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
-      s_exp[i] = c_gf8.exp[i];
       s_log[i] = c_gf8.log[i];
     }
   }
   __syncthreads();
-  const uint32_t MOD = GF16 ? 65535u : 255u;
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-    uint32_t acc = 0;
-    for (uint32_t e = 0; e < n; e++) {
-      if (pres[e]) continue;
-      const uint32_t x = i ^ e;
-      const uint32_t l = x == 0 ? 0u : (GF16 ? (uint32_t)glog[x] : (uint32_t)s_log[x]);
-      acc += l;
-      if (acc >= MOD) acc -= MOD;
+  // Error locator err[i] = sum_{e erased} log0[i ^ e] (mod MOD), an XOR convolution of
+  // the erasure indicator with log0: FWHT both, multiply pointwise, FWHT back and scale
+  // by 1/n = 2^(bits - log2 n) (2^bits = 1 mod MOD) - Leopard's own FWHT route, O(n log n)
+  // instead of the O(n^2) direct sum.
+  {
+    constexpr uint32_t MOD = GF16 ? 65535u : 255u;
+    constexpr uint32_t BITS = GF16 ? 16u : 8u;
+    uint32_t* tl = err + n;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+      err[i] = pres[i] ? 0u : 1u;
+      tl[i] = i == 0 ? 0u : (GF16 ? (uint32_t)glog[i] : (uint32_t)s_log[i]);
     }
-    err[i] = acc;
+    __syncthreads();
+    const uint32_t lgn = 31u - __builtin_clz(n);
+    auto fwht = [&](uint32_t* v0, uint32_t* v1) {
+      for (uint32_t lh = 0; lh < lgn; lh++) {
+        const uint32_t h = 1u << lh;
+        for (uint32_t j = threadIdx.x; j < n / 2; j += blockDim.x) {
+          const uint32_t a = ((j >> lh) << (lh + 1)) | (j & (h - 1)), b = a + h;
+          uint32_t x = v0[a], y = v0[b];
+          v0[a] = (x + y >= MOD) ? x + y - MOD : x + y;
+          v0[b] = (x >= y) ? x - y : x + MOD - y;
+          if (v1) {
+            x = v1[a];
+            y = v1[b];
+            v1[a] = (x + y >= MOD) ? x + y - MOD : x + y;
+            v1[b] = (x >= y) ? x - y : x + MOD - y;
+          }
+        }
+        __syncthreads();
+      }
+    };
+    fwht(err, tl);
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) err[i] = (err[i] * tl[i]) % MOD;
+    __syncthreads();
+    fwht(err, nullptr);
+    const uint32_t inv_n = (1u << (BITS - lgn)) % MOD;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) err[i] = (err[i] * inv_n) % MOD;
   }
   const uint32_t coff = blockIdx.y * 64u;
   for (uint32_t it = threadIdx.x; it < n * 4; it += blockDim.x) {
@@ -976,8 +1078,7 @@ __global__ __launch_bounds__(256) void k_rs_decode(uint8_t* shards, const uint8_
     Gf16Ops ops{gexp, glog};
     decode_chunk(ops, lds, err, pres, m, [&](uint32_t i) { return (uint32_t)gskew[i]; });
   } else {
-    Gf8Ops ops{s_exp, s_log};
-    decode_chunk(ops, lds, err, pres, m, [&](uint32_t i) { return (uint32_t)c_gf8.skew[i]; });
+    decode_chunk_gf8p(lds, err, pres, m, ltw, lmul);
   }
   for (uint32_t it = threadIdx.x; it < n * 4; it += blockDim.x) {
     const uint32_t p = it >> 2, q = it & 3;
@@ -995,7 +1096,7 @@ hipError_t launch_rs_decode(uint8_t* shards, const uint8_t* present, uint32_t na
   hipError_t e = ensure_gf8_const();
   if (e != hipSuccess) return e;
   const uint32_t n = 2 * m;
-  const size_t lds = (size_t)n * 64 + (size_t)n * 4 + n;
+  const size_t lds = (size_t)n * 64 + (size_t)n * 8 + n + (2 * m <= 256 ? (255 + 256) * 5 * 4 : 0);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   dim3 grid(naxes, len / 64);
   if (lds > 64 * 1024) {
@@ -1004,10 +1105,10 @@ hipError_t launch_rs_decode(uint8_t* shards, const uint8_t* present, uint32_t na
   }
   if (2 * m <= 256)
     hipLaunchKernelGGL(k_rs_decode<false>, grid, dim3(256), lds, s, shards, present, m, len, t.exp16, t.log16,
-                       t.skew16);
+                       t.skew16, t.tw8, t.mul8);
   else
     hipLaunchKernelGGL(k_rs_decode<true>, grid, dim3(256), lds, s, shards, present, m, len, t.exp16, t.log16,
-                       t.skew16);
+                       t.skew16, t.tw8, t.mul8);
   return hipGetLastError();
 }
 

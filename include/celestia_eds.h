@@ -182,6 +182,12 @@ cel_status cel_dah_hash(cel_ctx* ctx, const uint8_t* row_roots, const uint8_t* c
 cel_status cel_repair(cel_ctx* ctx, uint8_t* eds, uint8_t* present, uint32_t k,
                       uint32_t share_size, const uint8_t* row_roots, const uint8_t* col_roots,
                       int32_t* bad_axis, int32_t* bad_index);
+/* Same repair over an EDS resident on ctx's device (d_eds: 2k*2k*512 bytes, filled in
+ * place); present and the roots stay host memory (the crossword control loop runs on
+ * the host over the presence mask). Synchronous. */
+cel_status cel_dev_repair(cel_ctx* ctx, void* d_eds, uint8_t* present, uint32_t k,
+                          const uint8_t* row_roots, const uint8_t* col_roots, int32_t* bad_axis,
+                          int32_t* bad_index);
 
 /* ------------------------------------------------------- exported trees, proofs
  * pkg/proof (proof.go:78-202, row_proof.go, share_proof.go) and the subtree-root

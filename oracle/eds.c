@@ -260,7 +260,24 @@ int orc_repair(uint8_t* eds, uint8_t* present, uint32_t k, size_t share, const u
                const uint8_t* col_roots, int32_t* bad_axis, int32_t* bad_index) {
   orc_init();
   uint32_t w = 2 * k;
-  /* Verify complete axes first (rsmt2d checks roots of axes it did not solve too). */
+  size_t row = (size_t)w * share;
+  /* rsmt2d prerepairSanityCheck: axes complete before the repair must match their
+   * roots (rows, then columns, in index order). */
+  for (int is_col = 0; is_col < 2; is_col++)
+    for (uint32_t i = 0; i < w; i++) {
+      uint32_t have = 0;
+      for (uint32_t j = 0; j < w; j++) have += present[is_col ? (size_t)j * w + i : (size_t)i * w + j] ? 1 : 0;
+      if (have != w) continue;
+      uint8_t r[ORC_NODE];
+      if (is_col) orc_axis_root(eds + (size_t)i * share, row, k, i, share, r, 0);
+      else orc_axis_root(eds + (size_t)i * row, share, k, i, share, r, 0);
+      if (memcmp(r, (is_col ? col_roots : row_roots) + (size_t)i * ORC_NODE, ORC_NODE) != 0) {
+        if (bad_axis) *bad_axis = is_col;
+        if (bad_index) *bad_index = (int32_t)i;
+        return ORC_EBYZANTINE;
+      }
+    }
+  /* crossword: all rows, then all columns, until solved or stuck */
   for (;;) {
     int progress = 0;
     for (int is_col = 0; is_col < 2; is_col++)
@@ -280,7 +297,6 @@ int orc_repair(uint8_t* eds, uint8_t* present, uint32_t k, size_t share, const u
     if (!progress) return ORC_EUNREPAIRABLE;
   }
   /* Final consistency: every axis root must match. */
-  size_t row = (size_t)w * share;
   for (int is_col = 0; is_col < 2; is_col++)
     for (uint32_t i = 0; i < w; i++) {
       uint8_t r[ORC_NODE];

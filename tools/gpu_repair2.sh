@@ -1,0 +1,11 @@
+#!/bin/bash
+set -u
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_gpu_repair.py tests/test_gpu_codec.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_repair2.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_repair2.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 200 python3 bench.py --mode repair --steps 10 > gpurun_out/bench_repair_dev2.log 2>&1 || exit 1
+tail -1 gpurun_out/bench_repair_dev2.log
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_repair2 -o run --output-format csv -- python3 bench.py --mode repair --steps 5 --cpu-seconds 0.1 > /dev/null 2>&1; echo "prof rc=$?"
+python3 tools/kstats.py gpurun_out/prof_repair2
