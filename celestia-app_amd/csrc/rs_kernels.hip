@@ -932,62 +932,105 @@ __device__ void decode_chunk(const Ops& ops, uint32_t* lds, uint32_t* err, const
 
 // GF(2^8) decode of one 64-byte chunk with v_perm product tables staged in LDS
 // (ltw: twiddle tables by skew index, lmul: tables by log value; 5 dwords each) in
-// place of the per-byte log/exp lookups of Gf8Ops: same transform as decode_chunk,
-// with shift-only butterfly indexing.
+// place of the per-byte log/exp lookups of Gf8Ops: same transform as decode_chunk.
+// Layers go two at a time (radix 4: a thread owns one dword of four points, half the
+// LDS round trips and barriers of radix 2); the formal derivative reads every source
+// before one barrier and writes after it.
 __device__ void decode_chunk_gf8p(uint32_t* lds, const uint32_t* err, const uint8_t* pres, uint32_t m,
                                   const uint32_t* ltw, const uint32_t* lmul) {
   const uint32_t n = 2 * m;
   const uint32_t lgn = 31u - __builtin_clz(n);
   constexpr uint32_t U = 16;  // dwords per 64-byte chunk
   auto tab = [](const uint32_t* t) { return PermTab{t[0], t[1], t[2], t[3], t[4]}; };
+  // x ^= c(idx) * y, skipped for the zero twiddle
+  auto mad = [&](uint32_t& x, uint32_t y, uint32_t idx) {
+    if (c_gf8.skew[idx] != 255u) x ^= gf8_mul4(y, tab(ltw + idx * 5));
+  };
   for (uint32_t it = threadIdx.x; it < n * U; it += blockDim.x) {
     const uint32_t i = it / U, u = it % U;
     if (pres[i]) lds[i * 16 + u] = gf8_mul4(lds[i * 16 + u], tab(lmul + err[i] * 5));
   }
   __syncthreads();
-  const uint32_t items = (n / 2) * U;
-  for (uint32_t lD = 0; lD < lgn; lD++) {  // IFFT, offset 0
+  // IFFT (offset 0): layers D = 1, 2, 4, ...; butterfly y ^= x; x ^= c*y
+  uint32_t lD = 0;
+  for (; lD + 1 < lgn; lD += 2) {
     const uint32_t D = 1u << lD;
-    for (uint32_t it = threadIdx.x; it < items; it += blockDim.x) {
-      const uint32_t pair = it / U, u = it % U;
-      const uint32_t base = (pair >> lD) << (lD + 1), a = base + (pair & (D - 1));
-      uint32_t* x = lds + a * 16 + u;
-      uint32_t* y = lds + (a + D) * 16 + u;
-      const uint32_t idx = base + D - 1;
-      const uint32_t yv = *y ^ *x;
-      *y = yv;
-      if (c_gf8.skew[idx] != 255u) *x ^= gf8_mul4(yv, tab(ltw + idx * 5));
+    for (uint32_t it = threadIdx.x; it < (n / 4) * U; it += blockDim.x) {
+      const uint32_t q = it / U, u = it % U;
+      const uint32_t b4 = (q >> lD) << (lD + 2), a = b4 + (q & (D - 1));
+      uint32_t* p = lds + a * 16 + u;
+      uint32_t v0 = p[0], v1 = p[D * 16], v2 = p[2 * D * 16], v3 = p[3 * D * 16];
+      v1 ^= v0; mad(v0, v1, b4 + D - 1);
+      v3 ^= v2; mad(v2, v3, b4 + 3 * D - 1);
+      v2 ^= v0; mad(v0, v2, b4 + 2 * D - 1);
+      v3 ^= v1; mad(v1, v3, b4 + 2 * D - 1);
+      p[0] = v0; p[D * 16] = v1; p[2 * D * 16] = v2; p[3 * D * 16] = v3;
     }
     __syncthreads();
   }
-  // formal derivative (see decode_chunk)
-  for (uint32_t base = 0; base < n * U; base += blockDim.x) {
-    const uint32_t it = base + threadIdx.x;
-    uint32_t acc = 0;
-    const bool active = it < n * U;
-    uint32_t x = 0, u = 0;
-    if (active) {
-      x = it / U;
-      u = it % U;
-      for (uint32_t t = 1; t < n; t <<= 1)
-        if ((x & t) == 0 && x + t < n) acc ^= lds[(x + t) * 16 + u];
-    }
-    __syncthreads();
-    if (active) lds[x * 16 + u] ^= acc;
-    __syncthreads();
-  }
-  for (uint32_t lD = lgn; lD-- > 0;) {  // FFT
+  if (lD < lgn) {  // odd log2(n): one radix-2 layer left
     const uint32_t D = 1u << lD;
-    for (uint32_t it = threadIdx.x; it < items; it += blockDim.x) {
+    for (uint32_t it = threadIdx.x; it < (n / 2) * U; it += blockDim.x) {
       const uint32_t pair = it / U, u = it % U;
       const uint32_t base = (pair >> lD) << (lD + 1), a = base + (pair & (D - 1));
-      uint32_t* x = lds + a * 16 + u;
-      uint32_t* y = lds + (a + D) * 16 + u;
-      const uint32_t idx = base + D - 1;
-      uint32_t xv = *x;
-      if (c_gf8.skew[idx] != 255u) xv ^= gf8_mul4(*y, tab(ltw + idx * 5));
-      *x = xv;
-      *y ^= xv;
+      uint32_t x = lds[a * 16 + u], y = lds[(a + D) * 16 + u];
+      y ^= x;
+      mad(x, y, base + D - 1);
+      lds[a * 16 + u] = x;
+      lds[(a + D) * 16 + u] = y;
+    }
+    __syncthreads();
+  }
+  {  // formal derivative: new[x] = old[x] ^ xor_{t: bit t of x clear, x + 2^t < n} old[x + 2^t]
+    constexpr uint32_t kMaxItems = 256 * 16 / 256;  // GF(2^8): n <= 256 points, 256 threads
+    uint32_t acc[kMaxItems];
+#pragma unroll
+    for (uint32_t r = 0; r < kMaxItems; r++) {
+      const uint32_t it = threadIdx.x + r * 256u;
+      acc[r] = 0;
+      if (it < n * U) {
+        const uint32_t x = it / U, u = it % U;
+        for (uint32_t t = 1; t < n; t <<= 1)
+          if ((x & t) == 0 && x + t < n) acc[r] ^= lds[(x + t) * 16 + u];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t r = 0; r < kMaxItems; r++) {
+      const uint32_t it = threadIdx.x + r * 256u;
+      if (it < n * U) lds[(it / U) * 16 + it % U] ^= acc[r];
+    }
+    __syncthreads();
+  }
+  // FFT: layers D = n/2, ..., 1; butterfly x ^= c*y; y ^= x
+  lD = lgn;
+  if (lgn & 1) {  // odd log2(n): the top layer alone
+    lD = lgn - 1;
+    const uint32_t D = 1u << lD;
+    for (uint32_t it = threadIdx.x; it < (n / 2) * U; it += blockDim.x) {
+      const uint32_t pair = it / U, u = it % U;
+      const uint32_t base = (pair >> lD) << (lD + 1), a = base + (pair & (D - 1));
+      uint32_t x = lds[a * 16 + u], y = lds[(a + D) * 16 + u];
+      mad(x, y, base + D - 1);
+      y ^= x;
+      lds[a * 16 + u] = x;
+      lds[(a + D) * 16 + u] = y;
+    }
+    __syncthreads();
+  }
+  while (lD >= 2) {
+    lD -= 2;  // layers 2D then D
+    const uint32_t D = 1u << lD;
+    for (uint32_t it = threadIdx.x; it < (n / 4) * U; it += blockDim.x) {
+      const uint32_t q = it / U, u = it % U;
+      const uint32_t b4 = (q >> lD) << (lD + 2), a = b4 + (q & (D - 1));
+      uint32_t* p = lds + a * 16 + u;
+      uint32_t v0 = p[0], v1 = p[D * 16], v2 = p[2 * D * 16], v3 = p[3 * D * 16];
+      mad(v0, v2, b4 + 2 * D - 1); v2 ^= v0;
+      mad(v1, v3, b4 + 2 * D - 1); v3 ^= v1;
+      mad(v0, v1, b4 + D - 1); v1 ^= v0;
+      mad(v2, v3, b4 + 3 * D - 1); v3 ^= v2;
+      p[0] = v0; p[D * 16] = v1; p[2 * D * 16] = v2; p[3 * D * 16] = v3;
     }
     __syncthreads();
   }
@@ -1067,24 +1110,29 @@ __global__ __launch_bounds__(256) void k_rs_decode(uint8_t* shards, const uint8_
     const uint32_t inv_n = (1u << (BITS - lgn)) % MOD;
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) err[i] = (err[i] * inv_n) % MOD;
   }
-  const uint32_t coff = blockIdx.y * 64u;
-  for (uint32_t it = threadIdx.x; it < n * 4; it += blockDim.x) {
-    const uint32_t p = it >> 2, q = it & 3;
-    const uint32_t r = p < m ? m + p : p - m;
-    reinterpret_cast<uint4*>(lds)[it] = reinterpret_cast<const uint4*>(axis + (uint64_t)r * len + coff)[q];
-  }
-  __syncthreads();
-  if (GF16) {
-    Gf16Ops ops{gexp, glog};
-    decode_chunk(ops, lds, err, pres, m, [&](uint32_t i) { return (uint32_t)gskew[i]; });
-  } else {
-    decode_chunk_gf8p(lds, err, pres, m, ltw, lmul);
-  }
-  for (uint32_t it = threadIdx.x; it < n * 4; it += blockDim.x) {
-    const uint32_t p = it >> 2, q = it & 3;
-    if (pres[p]) continue;
-    const uint32_t r = p < m ? m + p : p - m;
-    reinterpret_cast<uint4*>(axis + (uint64_t)r * len + coff)[q] = reinterpret_cast<const uint4*>(lds)[it];
+  // the error locator and the staged tables serve every 64-byte chunk of the axis this
+  // workgroup takes (chunks blockIdx.y, blockIdx.y + gridDim.y, ...)
+  for (uint32_t chunk = blockIdx.y; chunk < len / 64u; chunk += gridDim.y) {
+    const uint32_t coff = chunk * 64u;
+    __syncthreads();  // the previous chunk's stores have read the LDS image
+    for (uint32_t it = threadIdx.x; it < n * 4; it += blockDim.x) {
+      const uint32_t p = it >> 2, q = it & 3;
+      const uint32_t r = p < m ? m + p : p - m;
+      reinterpret_cast<uint4*>(lds)[it] = reinterpret_cast<const uint4*>(axis + (uint64_t)r * len + coff)[q];
+    }
+    __syncthreads();
+    if (GF16) {
+      Gf16Ops ops{gexp, glog};
+      decode_chunk(ops, lds, err, pres, m, [&](uint32_t i) { return (uint32_t)gskew[i]; });
+    } else {
+      decode_chunk_gf8p(lds, err, pres, m, ltw, lmul);
+    }
+    for (uint32_t it = threadIdx.x; it < n * 4; it += blockDim.x) {
+      const uint32_t p = it >> 2, q = it & 3;
+      if (pres[p]) continue;
+      const uint32_t r = p < m ? m + p : p - m;
+      reinterpret_cast<uint4*>(axis + (uint64_t)r * len + coff)[q] = reinterpret_cast<const uint4*>(lds)[it];
+    }
   }
 }
 
@@ -1098,7 +1146,15 @@ hipError_t launch_rs_decode(uint8_t* shards, const uint8_t* present, uint32_t na
   const uint32_t n = 2 * m;
   const size_t lds = (size_t)n * 64 + (size_t)n * 8 + n + (2 * m <= 256 ? (255 + 256) * 5 * 4 : 0);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  dim3 grid(naxes, len / 64);
+  // chunks per workgroup (CEL_DEC_CPW, default 2): the per-axis setup (error locator,
+  // table staging) is shared by that many 64-byte chunks
+  static const uint32_t cpw = [] {
+    const char* e = getenv("CEL_DEC_CPW");
+    const int v = e ? atoi(e) : 2;
+    return (uint32_t)(v < 1 ? 1 : v);
+  }();
+  const uint32_t nch = len / 64;
+  dim3 grid(naxes, (nch + cpw - 1) / cpw);
   if (lds > 64 * 1024) {
     (void)hipFuncSetAttribute((const void*)k_rs_decode<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     (void)hipFuncSetAttribute((const void*)k_rs_decode<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
