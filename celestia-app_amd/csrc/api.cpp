@@ -188,6 +188,25 @@ static void pipe_plan(uint32_t n, uint32_t* chunk, uint32_t* nchunks) {
   *nchunks = (n + *chunk - 1) / *chunk;
 }
 
+// Chunks of the host-buffer pipeline (CEL_HOST_CHUNKS, default 4).
+static uint32_t host_chunks() {
+  static const uint32_t v = [] {
+    const char* e = getenv("CEL_HOST_CHUNKS");
+    const int x = e ? atoi(e) : 4;
+    return (uint32_t)(x < 1 ? 1 : (x > cel_ctx::kChunks ? cel_ctx::kChunks : x));
+  }();
+  return v;
+}
+
+void* cel_host_alloc(size_t bytes) {
+  void* p = nullptr;
+  return hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) == hipSuccess ? p : nullptr;
+}
+
+void cel_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
+
 size_t cel_dev_workspace_size(uint32_t k, uint32_t n) {
   uint32_t chunk, nchunks;
   pipe_plan(n, &chunk, &nchunks);
@@ -291,9 +310,19 @@ cel_status cel_extend_batch(cel_ctx* ctx, const uint8_t* ods, uint32_t n, uint32
   const size_t ods_b = (size_t)n * k * k * kShare, eds_b = 4 * ods_b;
   const size_t roots_b = (size_t)n * 2 * k * kNode;
   hipError_t e = hipSuccess;
+  // Chunked host pipeline: chunk c goes through upload (ODS into Q0) -> extension ->
+  // commit -> download on internal stream c % kPipe, so the PCIe copies of one chunk
+  // overlap the kernels and copies of the others (the copies dominate: 40 MiB of
+  // PCIe traffic per k=128 square against ~50 us of kernels). Host buffers from
+  // cel_host_alloc (pinned) make every copy asynchronous.
+  const uint32_t nc = std::min<uint32_t>(n, host_chunks());
+  const uint32_t chunk = (n + nc - 1) / nc;
+  const uint32_t nchunks = (n + chunk - 1) / chunk;
+  const uint32_t nstreams = std::min<uint32_t>(nchunks, cel_ctx::kPipe);
+  const size_t ws = nmt_workspace_size(k, chunk);
   uint8_t* d_eds = static_cast<uint8_t*>(scratch(ctx, S_EDS, eds_b, &e));
   if (!d_eds) return fail(ctx, CEL_ENOMEM, "device allocation failed");
-  void* d_work = scratch(ctx, S_WORK, cel_dev_workspace_size(k, n), &e);
+  uint8_t* d_work = static_cast<uint8_t*>(scratch(ctx, S_WORK, nstreams * ws, &e));
   if (!d_work) return fail(ctx, CEL_ENOMEM, "device allocation failed");
   uint8_t* d_out = static_cast<uint8_t*>(scratch(ctx, S_ROOTS, 2 * roots_b + (size_t)n * 32 + (size_t)n * 4, &e));
   if (!d_out) return fail(ctx, CEL_ENOMEM, "device allocation failed");
@@ -301,19 +330,43 @@ cel_status cel_extend_batch(cel_ctx* ctx, const uint8_t* ods, uint32_t n, uint32
   uint8_t* d_cr = d_out + roots_b;
   uint8_t* d_dah = d_out + 2 * roots_b;
   int32_t* d_st = reinterpret_cast<int32_t*>(d_out + 2 * roots_b + (size_t)n * 32);
-  hipStream_t s = ctx->stream;
-  // the upload places every ODS in Q0 of its EDS; the extension reads it in place
-  if ((e = place_ods(ods, n, k, d_eds, s)) != hipSuccess) return hip_fail(ctx, e, "H2D");
-  st = cel_dev_extend_batch(ctx, nullptr, n, k, d_eds, d_rr, d_cr, d_dah, d_st, d_work, s, flags);
-  if (st) return st;
-  if (eds_out && (e = hipMemcpyAsync(eds_out, d_eds, eds_b, hipMemcpyDeviceToHost, s)) != hipSuccess)
-    return hip_fail(ctx, e, "D2H");
   std::vector<int32_t> stv(n);
-  if ((e = hipMemcpyAsync(row_roots, d_rr, roots_b, hipMemcpyDeviceToHost, s)) != hipSuccess ||
-      (e = hipMemcpyAsync(col_roots, d_cr, roots_b, hipMemcpyDeviceToHost, s)) != hipSuccess ||
-      (e = hipMemcpyAsync(dah, d_dah, (size_t)n * 32, hipMemcpyDeviceToHost, s)) != hipSuccess ||
-      (e = hipMemcpyAsync(stv.data(), d_st, (size_t)n * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
-    return hip_fail(ctx, e, "D2H");
+  hipStream_t s = ctx->stream;
+  const uint64_t ods_sq = (uint64_t)k * k * kShare, eds_sq = 4 * ods_sq, roots_sq = (uint64_t)2 * k * kNode;
+  if ((e = hipEventRecord(ctx->ev_start, s)) != hipSuccess) return hip_fail(ctx, e, "event");
+  for (uint32_t c = 0; c < nchunks; c++) {
+    const uint32_t first = c * chunk, cnt = (first + chunk <= n) ? chunk : n - first;
+    hipStream_t cs = ctx->sub[c % cel_ctx::kPipe];
+    uint8_t* eds_c = d_eds + first * eds_sq;
+    if ((e = hipStreamWaitEvent(cs, ctx->ev_start, 0)) != hipSuccess ||
+        (e = place_ods(ods + first * ods_sq, cnt, k, eds_c, cs)) != hipSuccess ||
+        (e = launch_extend(nullptr, eds_c, k, cnt, ctx->tables, cs)) != hipSuccess ||
+        (e = launch_commit(eds_c, k, cnt, d_rr + first * roots_sq, d_cr + first * roots_sq, d_dah + first * 32,
+                           d_st + first, d_work + (c % cel_ctx::kPipe) * ws, (flags & CEL_FLAG_ORDER_CHECK) != 0,
+                           cs)) != hipSuccess)
+      return hip_fail(ctx, e, "extend batch");
+  }
+  // Downloads after every chunk is enqueued: a copy into pageable memory blocks the
+  // calling thread, and the later chunks' kernels run meanwhile.
+  for (uint32_t c = 0; c < nchunks; c++) {
+    const uint32_t first = c * chunk, cnt = (first + chunk <= n) ? chunk : n - first;
+    hipStream_t cs = ctx->sub[c % cel_ctx::kPipe];
+    uint8_t* eds_c = d_eds + first * eds_sq;
+    if ((eds_out && (e = hipMemcpyAsync(eds_out + first * eds_sq, eds_c, cnt * eds_sq, hipMemcpyDeviceToHost, cs)) !=
+                        hipSuccess) ||
+        (e = hipMemcpyAsync(row_roots + first * roots_sq, d_rr + first * roots_sq, cnt * roots_sq,
+                            hipMemcpyDeviceToHost, cs)) != hipSuccess ||
+        (e = hipMemcpyAsync(col_roots + first * roots_sq, d_cr + first * roots_sq, cnt * roots_sq,
+                            hipMemcpyDeviceToHost, cs)) != hipSuccess ||
+        (e = hipMemcpyAsync(dah + first * 32, d_dah + first * 32, (size_t)cnt * 32, hipMemcpyDeviceToHost, cs)) !=
+            hipSuccess ||
+        (e = hipMemcpyAsync(stv.data() + first, d_st + first, (size_t)cnt * 4, hipMemcpyDeviceToHost, cs)) !=
+            hipSuccess)
+      return hip_fail(ctx, e, "D2H");
+    if ((e = hipEventRecord(ctx->ev_done[c % cel_ctx::kChunks], cs)) != hipSuccess ||
+        (e = hipStreamWaitEvent(s, ctx->ev_done[c % cel_ctx::kChunks], 0)) != hipSuccess)
+      return hip_fail(ctx, e, "event");
+  }
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "sync");
   cel_status worst = CEL_OK;
   for (uint32_t i = 0; i < n; i++) {

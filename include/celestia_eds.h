@@ -88,6 +88,13 @@ cel_status cel_extend_batch(cel_ctx* ctx, const uint8_t* ods, uint32_t n, uint32
                             uint8_t* col_roots, uint8_t* dah, int32_t* status_out,
                             uint32_t flags);
 
+/* Page-locked host memory for the buffers of the host entry points (the ODS, the EDS
+ * output): with it every PCIe copy of cel_extend_batch is an asynchronous DMA that
+ * overlaps the other chunks' kernels. Any host memory works; pageable memory is
+ * staged by the runtime. cel_host_alloc returns NULL on failure. */
+void* cel_host_alloc(size_t bytes);
+void cel_host_free(void* p);
+
 /* -------------------------------------------------- square (device resident)
  * Same as cel_extend_batch with every pointer in device memory of ctx's device.
  * stream: a hipStream_t (NULL = ctx's own stream). Asynchronous: returns after
