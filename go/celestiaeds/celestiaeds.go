@@ -249,3 +249,52 @@ func (c *Context) GetCommitment(eds []byte, k, start, blobShareLen, subtreeRootT
 	}
 	return out, nil
 }
+
+// ByzantineError carries the axis (0 = row, 1 = column) and index rsmt2d's
+// ErrByzantineData reports; errors.Is(err, ErrByzantineData) holds.
+type ByzantineError struct {
+	Axis, Index int
+	msg         string
+}
+
+func (e *ByzantineError) Error() string { return e.msg }
+func (e *ByzantineError) Unwrap() error { return ErrByzantineData }
+
+// Repair wraps cel_repair, the device pass behind rsmt2d.ExtendedDataSquare.Repair:
+// flat is the flattened 2k x 2k square (missing cells may hold anything), present[i]
+// != 0 marks known cells. On success every cell of flat is filled in place.
+func (c *Context) Repair(flat, present []byte, k int, rowRoots, colRoots [][]byte) error {
+	w := 2 * k
+	rr := make([]byte, 0, w*NmtNodeSize)
+	cr := make([]byte, 0, w*NmtNodeSize)
+	for i := 0; i < w; i++ {
+		rr = append(rr, rowRoots[i]...)
+		cr = append(cr, colRoots[i]...)
+	}
+	var axis, index C.int32_t
+	c.mu.Lock()
+	st := C.cel_repair(c.ctx, (*C.uint8_t)(unsafe.Pointer(&flat[0])), (*C.uint8_t)(unsafe.Pointer(&present[0])),
+		C.uint32_t(k), ShareSize, (*C.uint8_t)(unsafe.Pointer(&rr[0])), (*C.uint8_t)(unsafe.Pointer(&cr[0])),
+		&axis, &index)
+	c.mu.Unlock()
+	if st == C.CEL_EBYZANTINE {
+		return &ByzantineError{Axis: int(axis), Index: int(index), msg: C.GoString(C.cel_last_error(c.ctx))}
+	}
+	return c.err(st)
+}
+
+// PinnedBuffer returns page-locked host memory (cel_host_alloc) for the flattened
+// ODS / EDS buffers of ExtendShares-style calls; free it with FreePinned.
+func PinnedBuffer(n int) []byte {
+	p := C.cel_host_alloc(C.size_t(n))
+	if p == nil {
+		return nil
+	}
+	return unsafe.Slice((*byte)(p), n)
+}
+
+func FreePinned(b []byte) {
+	if len(b) > 0 {
+		C.cel_host_free(unsafe.Pointer(&b[0]))
+	}
+}
