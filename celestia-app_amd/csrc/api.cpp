@@ -98,6 +98,9 @@ cel_status cel_ctx_create(int device, cel_ctx** out) {
     e = hipEventCreateWithFlags(&ctx->ev_done[i], hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_rs[i], hipEventDisableTiming);
   }
+  for (int i = 0; i <= cel_ctx::kChunks && e == hipSuccess; i++) {
+    e = hipEventCreateWithFlags(&ctx->ev_rows[i], hipEventDisableTiming);
+  }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_start, hipEventDisableTiming);
   if (e == hipSuccess) e = upload_tables(&ctx->tables);
   if (e != hipSuccess) {
@@ -121,6 +124,9 @@ void cel_ctx_destroy(cel_ctx* ctx) {
     for (int i = 0; i < cel_ctx::kChunks; i++) {
       if (ctx->ev_done[i]) (void)hipEventDestroy(ctx->ev_done[i]);
       if (ctx->ev_rs[i]) (void)hipEventDestroy(ctx->ev_rs[i]);
+    }
+    for (int i = 0; i <= cel_ctx::kChunks; i++) {
+      if (ctx->ev_rows[i]) (void)hipEventDestroy(ctx->ev_rows[i]);
     }
     if (ctx->ev_start) (void)hipEventDestroy(ctx->ev_start);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -247,8 +253,13 @@ cel_status cel_dev_extend_only(cel_ctx* ctx, const void* d_ods, uint32_t n, uint
   cel_status st = validate_square(ctx, k, kShare);
   if (st) return st;
   DeviceGuard g(ctx->device);
-  hipError_t e = launch_extend(static_cast<const uint8_t*>(d_ods), static_cast<uint8_t*>(d_eds), k, n, ctx->tables,
-                               pick_stream(ctx, stream));
+  const uint32_t m = extend_overlap_chunks();
+  hipStream_t us = pick_stream(ctx, stream);
+  hipError_t e = m ? launch_extend_2s(static_cast<const uint8_t*>(d_ods), static_cast<uint8_t*>(d_eds), k, n,
+                                      std::min<uint32_t>(m, cel_ctx::kChunks), ctx->tables, us,
+                                      ctx->sub[us == ctx->sub[0] ? 1 : 0], ctx->ev_rows)
+                   : launch_extend(static_cast<const uint8_t*>(d_ods), static_cast<uint8_t*>(d_eds), k, n,
+                                   ctx->tables, us);
   return e == hipSuccess ? CEL_OK : hip_fail(ctx, e, "extend");
 }
 

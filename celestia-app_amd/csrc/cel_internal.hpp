@@ -77,6 +77,11 @@ hipError_t launch_rs_encode_axis_segs(const RsGeom* gs, uint32_t nseg, hipStream
 // ods == nullptr means Q0 is already in place inside eds.
 hipError_t launch_extend(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t nsq,
                          const DeviceTables& t, hipStream_t s);
+// The same extension as m chunks over two streams: rows(c + 1) runs beside cols(c)
+// (an HBM-bound launch beside a VALU-bound one). ev: m + 1 events. s0 ends joined.
+hipError_t launch_extend_2s(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t nsq, uint32_t m,
+                            const DeviceTables& t, hipStream_t s0, hipStream_t s1, hipEvent_t* ev);
+uint32_t extend_overlap_chunks();
 
 // NMT + DAH over resident EDSs. work: scratch of nmt_workspace_size(k, nsq) bytes.
 size_t nmt_workspace_size(uint32_t k, uint32_t nsq);
@@ -149,6 +154,7 @@ struct cel_ctx {
   hipEvent_t ev_start = nullptr;
   hipEvent_t ev_done[kChunks] = {};
   hipEvent_t ev_rs[kChunks] = {};
+  hipEvent_t ev_rows[kChunks + 1] = {};  // two-stream extension: rows(c) done / join
   std::mutex mu;
   cel::DeviceTables tables;
   std::string last_error;

@@ -843,6 +843,42 @@ static hipError_t launch_extend_axis(const uint8_t* ods, uint8_t* eds, uint32_t 
   return hipSuccess;
 }
 
+// Chunks of the two-stream extension (CEL_RS_OVERLAP; 0 or 1 = off).
+uint32_t extend_overlap_chunks() {
+  static const int v = [] {
+    const char* e = getenv("CEL_RS_OVERLAP");
+    return e ? atoi(e) : 0;
+  }();
+  return v > 1 ? (uint32_t)v : 0u;
+}
+
+hipError_t launch_extend_2s(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t nsq, uint32_t m,
+                            const DeviceTables& t, hipStream_t s0, hipStream_t s1, hipEvent_t* ev) {
+  if (m > nsq) m = nsq;
+  if (m < 2) return launch_extend(ods, eds, k, nsq, t, s0);
+  const uint32_t chunk = (nsq + m - 1) / m;
+  m = (nsq + chunk - 1) / chunk;
+  hipError_t e;
+  if ((e = hipEventRecord(ev[m], s0)) != hipSuccess || (e = hipStreamWaitEvent(s1, ev[m], 0)) != hipSuccess) return e;
+  for (uint32_t c = 0; c < m; c++) {
+    const uint32_t first = c * chunk, n = (first + chunk <= nsq) ? chunk : nsq - first;
+    hipStream_t sc = (c & 1) ? s1 : s0;
+    // rows(c) starts once rows(c - 1) is done, i.e. beside cols(c - 1) on the other stream
+    if (c > 0 && (e = hipStreamWaitEvent(sc, ev[c - 1], 0)) != hipSuccess) return e;
+    const ExtGeoms x = ext_geoms(ods, eds, k, first, n);
+    if ((e = launch_rs_encode(x.rows, t, sc)) != hipSuccess) return e;
+    if ((e = hipEventRecord(ev[c], sc)) != hipSuccess) return e;
+    RsGeom cols = x.cols0;  // all 2k columns of [Q0|Q1] in one geometry (in place)
+    cols.in = eds + (uint64_t)first * 4 * k * k * kShare;
+    cols.in_sq = (uint64_t)4 * k * k * kShare;
+    cols.in_shard = (uint64_t)2 * k * kShare;
+    cols.axes = 2 * k;
+    if ((e = launch_rs_encode(cols, t, sc)) != hipSuccess) return e;
+  }
+  if ((e = hipEventRecord(ev[m], s1)) != hipSuccess) return e;
+  return hipStreamWaitEvent(s0, ev[m], 0);
+}
+
 hipError_t launch_extend(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t nsq, const DeviceTables& t,
                          hipStream_t s) {
   if (nsq == 0) return hipSuccess;
