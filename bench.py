@@ -61,7 +61,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--k", type=int, default=128, help="original square width")
-    ap.add_argument("--batch", type=int, default=128, help="squares per step per GPU")
+    ap.add_argument("--batch", type=int, default=256, help="squares per step per GPU")
     ap.add_argument("--distinct", type=int, default=4, help="distinct synthetic squares per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")

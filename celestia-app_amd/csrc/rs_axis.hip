@@ -165,6 +165,156 @@ __device__ __forceinline__ void transform(uint32_t (&w)[K]) {
   }
 }
 
+// ---------------------------------------------------------------- hybrid transform
+//
+// Layers with D >= 8 have the same twiddle for all 8 shards of an aligned block
+// {8m .. 8m+7} (the skew index depends on base = a & ~(2D-1) only), so there the block
+// is bit-sliced in place: an 8x8 bit transpose in each byte lane of w[8m .. 8m+7] turns
+// "4 bytes of 8 shards" into 8 bit-planes, and a butterfly between blocks m and m+D/8 is
+// an 8x8 GF(2) matrix network of v_bitop3 xor3 ops (~2 per plane) instead of the v_perm
+// multiply (~10 VALU per dword). Layers D = 1, 2, 4 (twiddles differ inside a block) keep
+// the v_perm multiply. For K = 128: 6 v_perm layers, 7 bit-sliced layers, 32 transposes.
+
+// 8x8 bit transpose in each byte lane of w[O .. O+8) (an involution): dword j <-> plane j.
+// Bit-field inserts (v_bfi_b32 / v_bitop3 0xCA): shift + insert for each side, 4 VALU.
+template <int A, int B, int S, uint32_t M, int K>
+__device__ __forceinline__ void swapb(uint32_t (&w)[K]) {
+  const uint32_t a = w[A], b = w[B];
+  constexpr uint32_t MH = M << S;
+  w[B] = __builtin_amdgcn_bitop3_b32(M, a >> S, b, 0xCA);
+  w[A] = __builtin_amdgcn_bitop3_b32(MH, b << S, a, 0xCA);
+}
+template <int O, int K>
+__device__ __forceinline__ void tr8(uint32_t (&w)[K]) {
+  swapb<O + 0, O + 4, 4, 0x0F0F0F0Fu>(w);
+  swapb<O + 1, O + 5, 4, 0x0F0F0F0Fu>(w);
+  swapb<O + 2, O + 6, 4, 0x0F0F0F0Fu>(w);
+  swapb<O + 3, O + 7, 4, 0x0F0F0F0Fu>(w);
+  swapb<O + 0, O + 2, 2, 0x33333333u>(w);
+  swapb<O + 1, O + 3, 2, 0x33333333u>(w);
+  swapb<O + 4, O + 6, 2, 0x33333333u>(w);
+  swapb<O + 5, O + 7, 2, 0x33333333u>(w);
+  swapb<O + 0, O + 1, 1, 0x55555555u>(w);
+  swapb<O + 2, O + 3, 1, 0x55555555u>(w);
+  swapb<O + 4, O + 5, 1, 0x55555555u>(w);
+  swapb<O + 6, O + 7, 1, 0x55555555u>(w);
+}
+
+// acc ^= xor of w[YO + j] for every set bit j of ROW (two inputs per v_bitop3).
+template <uint32_t ROW, int YO, int J, int K>
+__device__ __forceinline__ void xrow(uint32_t& acc, const uint32_t (&w)[K]) {
+  if constexpr (J < 8) {
+    if constexpr ((ROW >> J) & 1u) {
+      constexpr uint32_t rest = ROW >> (J + 1);
+      if constexpr (rest != 0) {
+        constexpr int J2 = J + 1 + __builtin_ctz(rest);
+        acc = __builtin_amdgcn_bitop3_b32(acc, w[YO + J], w[YO + J2], 0x96);
+        xrow<ROW, YO, J2 + 1>(acc, w);
+      } else {
+        acc ^= w[YO + J];
+      }
+    } else {
+      xrow<ROW, YO, J + 1>(acc, w);
+    }
+  }
+}
+
+// planes w[XO..XO+8) ^= exp(LM) * planes w[YO..YO+8); LM == 255 is the zero twiddle.
+template <uint32_t LM, int XO, int YO, int K>
+__device__ __forceinline__ void pmuladd(uint32_t (&w)[K]) {
+  if constexpr (LM != 255u) {
+    sfor<8>([&](auto r) { xrow<cx::mul_row(LM, decltype(r)::value), YO, 0>(w[XO + decltype(r)::value], w); });
+  }
+}
+template <int XO, int YO, int K>
+__device__ __forceinline__ void pxor(uint32_t (&w)[K]) {
+#pragma unroll
+  for (int b = 0; b < 8; b++) w[YO + b] ^= w[XO + b];
+}
+
+template <int K>
+__device__ __forceinline__ void transform_hyb(uint32_t (&w)[K]) {
+  constexpr int LOGK = __builtin_ctz(K);
+  static_assert(K >= 32, "hybrid transform needs bit-sliced layers");
+  const uint32_t m7 = sconst<0x07070707u>(), m3 = sconst<0x03030303u>();
+  // IFFT D = 1, 2, 4: v_perm multiply
+  sfor<3>([&](auto lg) {
+    constexpr int D = 1 << decltype(lg)::value;
+    sfor<K / (2 * D)>([&](auto bi) {
+      constexpr int base = decltype(bi)::value * 2 * D;
+      const Mul<kGf8.skew[K - 1 + base + D]> m;
+      sfor<D>([&](auto j) {
+        constexpr int a = base + decltype(j)::value;
+        pin(w[a], w[a + D]);
+        w[a + D] ^= w[a];
+        m.muladd(w[a], w[a + D], m7, m3);
+        pin(w[a], w[a + D]);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    });
+  });
+  sfor<K / 8>([&](auto s) {
+    tr8<8 * decltype(s)::value>(w);
+    __builtin_amdgcn_sched_barrier(0);
+  });
+  // IFFT D = 8 .. K/4, bit-sliced (block pairs)
+  sfor<LOGK - 4>([&](auto t) {
+    constexpr int D = 8 << decltype(t)::value;
+    sfor<K / (2 * D)>([&](auto bi) {
+      constexpr int base = decltype(bi)::value * 2 * D;
+      sfor<D / 8>([&](auto j) {
+        constexpr int a = base + 8 * decltype(j)::value;
+        pxor<a, a + D>(w);
+        pmuladd<kGf8.skew[K - 1 + base + D], a, a + D>(w);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    });
+  });
+  {  // last IFFT layer + first FFT layer, merged (see transform)
+    constexpr int D = K / 2;
+    sfor<D / 8>([&](auto j) {
+      constexpr int a = 8 * decltype(j)::value;
+      pxor<a, a + D>(w);
+      pmuladd<merged_lm(kGf8.skew[K - 1 + D], kGf8.skew[D - 1]), a, a + D>(w);
+      pxor<a, a + D>(w);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  }
+  // FFT D = K/4 .. 8, bit-sliced
+  sfor<LOGK - 4>([&](auto t) {
+    constexpr int D = K >> (decltype(t)::value + 2);
+    sfor<K / (2 * D)>([&](auto bi) {
+      constexpr int base = decltype(bi)::value * 2 * D;
+      sfor<D / 8>([&](auto j) {
+        constexpr int a = base + 8 * decltype(j)::value;
+        pmuladd<kGf8.skew[base + D - 1], a, a + D>(w);
+        pxor<a, a + D>(w);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    });
+  });
+  sfor<K / 8>([&](auto s) {
+    tr8<8 * decltype(s)::value>(w);
+    __builtin_amdgcn_sched_barrier(0);
+  });
+  // FFT D = 4, 2, 1: v_perm multiply
+  sfor<3>([&](auto t) {
+    constexpr int D = 4 >> decltype(t)::value;
+    sfor<K / (2 * D)>([&](auto bi) {
+      constexpr int base = decltype(bi)::value * 2 * D;
+      const Mul<kGf8.skew[base + D - 1]> m;
+      sfor<D>([&](auto j) {
+        constexpr int a = base + decltype(j)::value;
+        pin(w[a], w[a + D]);
+        m.muladd(w[a], w[a + D], m7, m3);
+        w[a + D] ^= w[a];
+        pin(w[a], w[a + D]);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    });
+  });
+}
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
 }
@@ -175,7 +325,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
 // One launch covers up to kMaxSegs geometries (RsSegs) of the same n: tiles
 // [end[i-1], end[i]) belong to segment i. The extension pipeline (launch_extend_axis)
 // puts the last column pass of chunk c-1 and both Q0 passes of chunk c in one launch.
-template <int LOGK, int DBG>
+template <int LOGK, int DBG, bool HYB, int LDA = 0, int STA = 0>
 __global__ __launch_bounds__(256, 3) void k_rs_axis_gf8(RsSegs sg) {
   constexpr int K = 1 << LOGK;
   const uint32_t lane = threadIdx.x & 63;
@@ -203,15 +353,18 @@ __global__ __launch_bounds__(256, 3) void k_rs_axis_gf8(RsSegs sg) {
     const auto rin = rsrc(g.in + (uint64_t)z * g.in_sq + (uint64_t)x * g.in_axis + (uint64_t)y * 256u);
     const uint32_t in_shard = (uint32_t)g.in_shard;
 #pragma unroll
-    for (int i = 0; i < K; i++) w[i] = __builtin_amdgcn_raw_buffer_load_b32(rin, lo, (uint32_t)i * in_shard, 0);
+    for (int i = 0; i < K; i++) w[i] = __builtin_amdgcn_raw_buffer_load_b32(rin, lo, (uint32_t)i * in_shard, LDA);
     if (g.dcopy && active) {
       const auto rdc = rsrc(g.dcopy + (uint64_t)z * g.dc_sq + (uint64_t)x * g.dc_axis + (uint64_t)y * 256u);
       const uint32_t dc_shard = (uint32_t)g.dc_shard;
 #pragma unroll
-      for (int i = 0; i < K; i++) __builtin_amdgcn_raw_buffer_store_b32(w[i], rdc, lo, (uint32_t)i * dc_shard, 0);
+      for (int i = 0; i < K; i++) __builtin_amdgcn_raw_buffer_store_b32(w[i], rdc, lo, (uint32_t)i * dc_shard, STA);
     }
   }
-  if constexpr (DBG != 1) transform<K>(w);
+  if constexpr (DBG != 1) {
+    if constexpr (HYB) transform_hyb<K>(w);
+    else transform<K>(w);
+  }
   if constexpr (DBG == 2) {
     uint32_t acc = 0;
 #pragma unroll
@@ -221,18 +374,32 @@ __global__ __launch_bounds__(256, 3) void k_rs_axis_gf8(RsSegs sg) {
     const auto rout = rsrc(g.out + (uint64_t)z * g.out_sq + (uint64_t)x * g.out_axis + (uint64_t)y * 256u);
     const uint32_t out_shard = (uint32_t)g.out_shard;
 #pragma unroll
-    for (int i = 0; i < K; i++) __builtin_amdgcn_raw_buffer_store_b32(w[i], rout, lo, (uint32_t)i * out_shard, 0);
+    for (int i = 0; i < K; i++) __builtin_amdgcn_raw_buffer_store_b32(w[i], rout, lo, (uint32_t)i * out_shard, STA);
   }
 }
 
-template <int LOGK>
+// Buffer cache-policy bits of the loads/stores (CEL_RS_CP, A/B only): 0 default,
+// 1 nt stores, 2 nt loads and stores, 3 sc0|sc1 stores.
+static int rs_cache_policy() {
+  static const int v = [] {
+    const char* e = getenv("CEL_RS_CP");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+template <int LOGK, bool HYB>
 hipError_t launch(const RsSegs& sg, hipStream_t s, int dbg) {
   const uint32_t ntiles = sg.end[sg.nseg - 1];
   if (ntiles == 0) return hipSuccess;
   const dim3 grid((ntiles + 3) / 4);
-  if (dbg == 1) hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 1>), grid, dim3(256), 0, s, sg);
-  else if (dbg == 2) hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 2>), grid, dim3(256), 0, s, sg);
-  else hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 0>), grid, dim3(256), 0, s, sg);
+  const int cp = rs_cache_policy();
+  if (dbg == 1) hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 1, false>), grid, dim3(256), 0, s, sg);
+  else if (dbg == 2) hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 2, HYB>), grid, dim3(256), 0, s, sg);
+  else if (HYB && cp == 1) hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 0, HYB, 0, 2>), grid, dim3(256), 0, s, sg);
+  else if (HYB && cp == 2) hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 0, HYB, 2, 2>), grid, dim3(256), 0, s, sg);
+  else if (HYB && cp == 3) hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 0, HYB, 0, 17>), grid, dim3(256), 0, s, sg);
+  else hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 0, HYB>), grid, dim3(256), 0, s, sg);
   return hipGetLastError();
 }
 
@@ -244,6 +411,16 @@ static int rs_debug() {
     return e ? atoi(e) : 0;
   }();
   return dbg;
+}
+
+// Bit-sliced D >= 8 layers (transform_hyb) for n >= 32: CEL_RS_HYB=0 selects the
+// all-v_perm transform.
+static bool rs_hybrid() {
+  static const bool v = [] {
+    const char* e = getenv("CEL_RS_HYB");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return v;
 }
 
 // Byte offsets must fit the 32-bit buffer offsets: (n - 1) * shard stride + len < 2 GiB.
@@ -267,15 +444,16 @@ hipError_t launch_rs_encode_axis_segs(const RsGeom* gs, uint32_t nseg, hipStream
   }
   sg.nseg = nseg;
   const int dbg = rs_debug();
+  const bool hyb = rs_hybrid();
   switch (gs[0].n) {
-    case 1: return ax::launch<0>(sg, s, dbg);
-    case 2: return ax::launch<1>(sg, s, dbg);
-    case 4: return ax::launch<2>(sg, s, dbg);
-    case 8: return ax::launch<3>(sg, s, dbg);
-    case 16: return ax::launch<4>(sg, s, dbg);
-    case 32: return ax::launch<5>(sg, s, dbg);
-    case 64: return ax::launch<6>(sg, s, dbg);
-    case 128: return ax::launch<7>(sg, s, dbg);
+    case 1: return ax::launch<0, false>(sg, s, dbg);
+    case 2: return ax::launch<1, false>(sg, s, dbg);
+    case 4: return ax::launch<2, false>(sg, s, dbg);
+    case 8: return ax::launch<3, false>(sg, s, dbg);
+    case 16: return ax::launch<4, false>(sg, s, dbg);
+    case 32: return hyb ? ax::launch<5, true>(sg, s, dbg) : ax::launch<5, false>(sg, s, dbg);
+    case 64: return hyb ? ax::launch<6, true>(sg, s, dbg) : ax::launch<6, false>(sg, s, dbg);
+    case 128: return hyb ? ax::launch<7, true>(sg, s, dbg) : ax::launch<7, false>(sg, s, dbg);
     default: return hipErrorInvalidValue;
   }
 }
