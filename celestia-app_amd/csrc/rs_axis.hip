@@ -378,12 +378,14 @@ __global__ __launch_bounds__(256, 3) void k_rs_axis_gf8(RsSegs sg) {
   }
 }
 
-// Buffer cache-policy bits of the loads/stores (CEL_RS_CP, A/B only): 0 default,
-// 1 nt stores, 2 nt loads and stores, 3 sc0|sc1 stores.
+// Buffer cache-policy bits of the loads and stores. Default: nt (non-temporal) on both:
+// every byte is touched once per pass and the batch is far larger than the Infinity
+// Cache; k=128 B=256: 9.35 -> 9.00 us per square (profiles/r1d_rs_cache_policy_ab.txt).
+// CEL_RS_CP (A/B only): 0 default policy, 1 nt stores only, 3 sc0|sc1 stores.
 static int rs_cache_policy() {
   static const int v = [] {
     const char* e = getenv("CEL_RS_CP");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 2;
   }();
   return v;
 }
@@ -396,10 +398,10 @@ hipError_t launch(const RsSegs& sg, hipStream_t s, int dbg) {
   const int cp = rs_cache_policy();
   if (dbg == 1) hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 1, false>), grid, dim3(256), 0, s, sg);
   else if (dbg == 2) hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 2, HYB>), grid, dim3(256), 0, s, sg);
+  else if (cp == 0) hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 0, HYB>), grid, dim3(256), 0, s, sg);
   else if (HYB && cp == 1) hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 0, HYB, 0, 2>), grid, dim3(256), 0, s, sg);
-  else if (HYB && cp == 2) hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 0, HYB, 2, 2>), grid, dim3(256), 0, s, sg);
   else if (HYB && cp == 3) hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 0, HYB, 0, 17>), grid, dim3(256), 0, s, sg);
-  else hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 0, HYB>), grid, dim3(256), 0, s, sg);
+  else hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 0, HYB, 2, 2>), grid, dim3(256), 0, s, sg);
   return hipGetLastError();
 }
 

@@ -21,9 +21,11 @@ a = ap.parse_args()
 from celestia_eds.device import SquareBatch  # noqa: E402
 from celestia_eds.testfactory import random_ods  # noqa: E402
 
-sb = SquareBatch(a.batch, a.k)
+# --inplace: the random ODS sits in Q0 of every EDS (as in bench.py); the kernels'
+# power draw, and so the clock, depends on the data, so never time all-zero squares.
+sb = SquareBatch(a.batch, a.k, ods_in_eds=a.inplace)
 ods = random_ods(a.k, 1)
-sb.ods.copy_(torch.from_numpy(np.stack([ods] * a.batch)))
+sb.load_ods(torch.from_numpy(np.stack([ods] * a.batch)))
 c = sb.ctx
 k, B = a.k, a.batch
 ods_sq, eds_sq = k * k * 512, 4 * k * k * 512
