@@ -36,7 +36,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table)
 SHA_MIX_CEILING = 1024 * 2.4e9 * 64 / 4528
 # Measured HBM traffic of the RS extension (rocprofv3 FETCH_SIZE/WRITE_SIZE passes).
 # (input layout -> profile): ODS in Q0 of the EDS (in place) / separate ODS buffer.
-TRAFFIC_PROFILE = {"eds": "r1_rs_traffic_inplace.json", "ods": "r1_rs_traffic.json"}
+TRAFFIC_PROFILE = {"eds": "r1e_rs_traffic_inplace.json", "ods": "r1_rs_traffic.json"}
 
 
 def _rs_traffic(k, batch, layout):
