@@ -69,6 +69,9 @@ def parse():
                     help="eds: the upload places each ODS in Q0 of its EDS buffer and the extension "
                          "reads it in place; ods: separate contiguous ODS buffer, the row pass copies Q0")
     ap.add_argument("--phase-reps", type=int, default=10)
+    ap.add_argument("--k512-batch", type=int, default=8,
+                    help="with --k 128: k=512 squares per step per GPU of the companion line (0 = off)")
+    ap.add_argument("--k512-steps", type=int, default=5)
     ap.add_argument("--mode", default="batch", choices=["batch", "sharded", "repair"],
                     help="batch: independent squares per GPU (configs 2, 4); sharded: one square "
                          "row-sharded over the ranks (config 3); repair: rsmt2d Repair (config 5)")
@@ -277,6 +280,56 @@ def run_repair(a):
     }), flush=True)
 
 
+def _measure_batch(ctx, local, rank, k, B, steps, warmup, n_distinct, layout, phase_reps, barrier, dist, dev):
+    """Time `steps` batch steps of B k x k squares resident in HBM (barrier + synchronize
+    on both sides, max over ranks), then the RS and NMT phases alone with HIP events on
+    the batch's launch stream."""
+    from celestia_eds.device import SquareBatch
+    from celestia_eds.testfactory import random_ods
+
+    sb = SquareBatch(B, k, device=local, ctx=ctx, ods_in_eds=(layout == "eds"))
+    distinct = [random_ods(k, 1_000_003 * rank + i) for i in range(min(n_distinct, B))]
+    host = np.stack([distinct[i % len(distinct)] for i in range(B)])
+    sb.load_ods(torch.from_numpy(host))
+    del host
+    torch.cuda.synchronize()
+    for _ in range(warmup):
+        sb.extend_and_commit()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        sb.extend_and_commit()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    status = sb.status.cpu().numpy()
+    assert (status == 0).all(), f"device reported status {status}"
+
+    stream = sb.hip_stream  # the stream every launch of `sb` goes to
+
+    def timed(fn, reps):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        fn()
+        e0.record(stream)
+        for _ in range(reps):
+            fn()
+        e1.record(stream)
+        e1.synchronize()
+        return e0.elapsed_time(e1) / reps / 1e3  # seconds per launch
+
+    t_ext = timed(sb.extend_only, phase_reps)
+    t_com = timed(sb.commit_only, phase_reps)
+    return {"sb": sb, "distinct": distinct, "elapsed": elapsed, "t_ext": t_ext, "t_com": t_com}
+
+
 def main():
     a = parse()
     if a.mode == "sharded":
@@ -294,64 +347,24 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from celestia_eds import default_context
-    from celestia_eds.device import SquareBatch
-    from celestia_eds.testfactory import random_ods
 
     ctx = default_context(local)
-    k, B = a.k, a.batch
-    sb = SquareBatch(B, k, device=local, ctx=ctx, ods_in_eds=(a.input == "eds"))
-    distinct = [random_ods(k, 1_000_003 * rank + i) for i in range(min(a.distinct, B))]
-    host = np.stack([distinct[i % len(distinct)] for i in range(B)])
-    sb.load_ods(torch.from_numpy(host))
-    torch.cuda.synchronize()
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
-    for _ in range(a.warmup):
-        sb.extend_and_commit()
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        sb.extend_and_commit()
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    status = sb.status.cpu().numpy()
-    assert (status == 0).all(), f"device reported status {status}"
-
-    # ---- phase timing with HIP events on the launch stream (rank-local)
-    stream = sb.hip_stream  # the stream every launch of `sb` goes to
-
-    def timed(fn, reps):
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        fn()
-        e0.record(stream)
-        for _ in range(reps):
-            fn()
-        e1.record(stream)
-        e1.synchronize()
-        return e0.elapsed_time(e1) / reps / 1e3  # seconds per launch
-
-    t_ext = timed(sb.extend_only, a.phase_reps)
-    t_com = timed(sb.commit_only, a.phase_reps)
-
+    m = _measure_batch(ctx, local, rank, a.k, a.batch, a.steps, a.warmup, a.distinct, a.input,
+                       a.phase_reps, barrier, dist, dev)
+    k, B, elapsed, t_ext, t_com = a.k, a.batch, m["elapsed"], m["t_ext"], m["t_com"]
+    sb, distinct = m["sb"], m["distinct"]
+    del m
     squares = world * B * a.steps
     value = squares / elapsed
     ods_bytes = 512 * k * k
     rs_bytes = 2048 * k * k * B  # read ODS + write Q1..Q3, per launch pair
     rs_gbs = rs_bytes / t_ext / 1e9
     compressions = (60 * k * k + 4 * k - 2) * B
-    # ~1.5k VALU lane-ops per SHA-256 compression (fully unrolled)
     nmt_rate = compressions / t_com
 
     result = {
@@ -401,13 +414,38 @@ def main():
         },
     }
 
+    if a.k == 128 and a.k512_batch > 0:
+        # The metric names k=128 and k=512: a short GF(2^16) batch rides along with the
+        # headline k=128 line (same contract: barrier + max over ranks, whole job).
+        dah128 = sb.dah.cpu().numpy()
+        del sb
+        torch.cuda.empty_cache()
+        m5 = _measure_batch(ctx, local, rank, 512, a.k512_batch, a.k512_steps, 2, 2, a.input,
+                            3, barrier, dist, dev)
+        B5, t5 = a.k512_batch, m5["elapsed"]
+        v5 = world * B5 * a.k512_steps / t5
+        rs5 = 2048 * 512 * 512 * B5 / m5["t_ext"] / 1e9
+        comp5 = (60 * 512 * 512 + 4 * 512 - 2) * B5 / m5["t_com"]
+        result["k512"] = {
+            "workload": "k=512 ODS (GF(2^16)) -> EDS + 2048 NMT roots + DAH, batch replay",
+            "value": v5, "unit": "squares/s", "ods_gbps": v5 * 512 * 512 * 512 / 1e9,
+            "squares_per_step_per_gpu": B5, "steps": a.k512_steps,
+            "ms_per_step": t5 / a.k512_steps * 1e3,
+            "rs_frac_hbm": rs5 / HBM_PEAK_GBS, "rs_avg_launch_us": m5["t_ext"] * 1e6,
+            "nmt_frac_sha_mix": comp5 / SHA_MIX_CEILING, "nmt_avg_launch_us": m5["t_com"] * 1e6,
+        }
+        del m5
+        torch.cuda.empty_cache()
+        sb = None
+    else:
+        dah128 = None
     if rank == 0 and world == 1 and not a.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
         oracle.set_simd(True)
         oracle.set_threads(_cpu_cores())
         n_done, t_cpu = 0, 0.0
-        dah_dev = sb.dah.cpu().numpy()
+        dah_dev = dah128 if dah128 is not None else sb.dah.cpu().numpy()
         parity = True
         while t_cpu < a.cpu_seconds or n_done < 2:
             i = n_done % len(distinct)
