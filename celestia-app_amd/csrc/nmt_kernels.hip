@@ -81,6 +81,11 @@ __device__ __forceinline__ void put_digest(uint32_t (&nd)[kNodeWords], const uin
 // Message word at byte p >= 32 is share bytes q..q+3 with q = p - 30 (q = 2 mod 4):
 // bytes 2,3 of dword (q-2)/4 and bytes 0,1 of the next -> one v_perm_b32 (and the
 // byte swap to big-endian comes for free in the same select).
+// Parity cells: message bytes 0..27 are 0x00 || 0xFF*27 (ns = 0xFF*29 continues into w7).
+constexpr uint32_t kLeafParPrefix[7] = {0x00FFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu,
+                                        0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+constexpr ShaMid kLeafParMid = sha_midstate(kLeafParPrefix, 7);
+
 __device__ __forceinline__ void leaf_hash(uint32_t (&st)[8], const uint32_t* __restrict__ sh, bool q0) {
   sha256_init(st);
   uint32_t w[16];
@@ -90,20 +95,26 @@ __device__ __forceinline__ void leaf_hash(uint32_t (&st)[8], const uint32_t* __r
     const uint4 v0 = p4[0], v1 = p4[1];
     s[0] = v0.x; s[1] = v0.y; s[2] = v0.z; s[3] = v0.w; s[4] = v1.x; s[5] = v1.y; s[6] = v1.z; s[7] = v1.w;
     s[8] = sh[8];
-    if (q0) {
-      w[0] = perm(0u, s[0], 0x0C000102u);
-#pragma unroll
-      for (int i = 1; i < 7; i++) w[i] = perm(s[i - 1], s[i], 0x07000102u);
-      w[7] = perm(s[6], s[7], 0x07000C0Cu) | perm(0u, s[0], 0x0C0C0001u);
-    } else {
-      w[0] = 0x00FFFFFFu;
-#pragma unroll
-      for (int i = 1; i < 7; i++) w[i] = 0xFFFFFFFFu;
-      w[7] = 0xFFFF0000u | perm(0u, s[0], 0x0C0C0001u);
-    }
 #pragma unroll
     for (int i = 8; i < 16; i++) w[i] = perm(s[i - 8], s[i - 7], 0x06070001u);
-    sha256_compress(st, w);
+    if (__all(!q0)) {  // wave-uniform parity cells: rounds 0..6 are one constant
+#pragma unroll
+      for (int i = 0; i < 7; i++) w[i] = kLeafParPrefix[i];
+      w[7] = 0xFFFF0000u | perm(0u, s[0], 0x0C0C0001u);
+      sha256_compress_from<7>(st, mid_regs(kLeafParMid), w);
+    } else {
+      if (q0) {
+        w[0] = perm(0u, s[0], 0x0C000102u);
+#pragma unroll
+        for (int i = 1; i < 7; i++) w[i] = perm(s[i - 1], s[i], 0x07000102u);
+        w[7] = perm(s[6], s[7], 0x07000C0Cu) | perm(0u, s[0], 0x0C0C0001u);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 7; i++) w[i] = kLeafParPrefix[i];
+        w[7] = 0xFFFF0000u | perm(0u, s[0], 0x0C0C0001u);
+      }
+      sha256_compress(st, w);
+    }
   }
 #pragma unroll 1
   for (int b = 1; b < 8; b++) {  // blocks 1..7: share bytes [64b-30, 64b+34)
@@ -209,26 +220,49 @@ __global__ CEL_LEAF_BOUNDS void k_leaf(const uint8_t* __restrict__ eds, uint32_t
 
 // HashNode(L, R): message 0x01 || L(90) || R(90) = 181 B -> 3 blocks.
 // minNs = L.min; maxNs = (R.min == 0xFF*29) ? L.max : R.max  (IgnoreMaxNamespace).
+// Parity left child (min = max = 0xFF*29, nodes of Q1-Q3): message bytes 0..55 are
+// 0x01 || 0xFF*55 for every such node, so rounds 0..13 of block 0 are one constant.
+constexpr uint32_t kNodeParPrefix[14] = {0x01FFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu,
+                                         0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu,
+                                         0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+constexpr ShaMid kNodeParMid = sha_midstate(kNodeParPrefix, 14);
+
+__device__ __forceinline__ uint32_t node_word(const uint32_t (&L)[kNodeWords], const uint32_t (&R)[kNodeWords], int q) {
+  if (q == 0) return perm(1u, L[0], 0x04000102u);
+  if (q <= 21) return perm(L[q - 1], L[q], 0x07000102u);
+  if (q == 22) return perm(L[21], L[22], 0x0700010Cu) | (R[0] & 0xFFu);
+  if (q <= 44) return perm(R[q - 23], R[q - 22], 0x05060700u);
+  if (q == 45) return perm(R[22], 0x80u, 0x05000C0Cu);
+  if (q == 47) return 181u * 8u;
+  return 0u;
+}
+
 __device__ __forceinline__ void hash_node(const uint32_t (&L)[kNodeWords], const uint32_t (&R)[kNodeWords],
                                           uint32_t (&out)[kNodeWords]) {
   uint32_t st[8];
   sha256_init(st);
+  bool lpar = (L[14] & 0xFFFFu) == 0xFFFFu;
 #pragma unroll
-  for (int b = 0; b < 3; b++) {
+  for (int i = 0; i < 14; i++) lpar = lpar && (L[i] == 0xFFFFFFFFu);
+  {
+    uint32_t w[16];
+    if (__all(lpar)) {  // wave-uniform: the whole wave starts block 0 at round 14
+#pragma unroll
+      for (int wi = 0; wi < 14; wi++) w[wi] = kNodeParPrefix[wi];
+      w[14] = node_word(L, R, 14);
+      w[15] = node_word(L, R, 15);
+      sha256_compress_from<14>(st, mid_regs(kNodeParMid), w);
+    } else {
+#pragma unroll
+      for (int wi = 0; wi < 16; wi++) w[wi] = node_word(L, R, wi);
+      sha256_compress(st, w);
+    }
+  }
+#pragma unroll
+  for (int b = 1; b < 3; b++) {
     uint32_t w[16];
 #pragma unroll
-    for (int wi = 0; wi < 16; wi++) {
-      const int q = 16 * b + wi;
-      uint32_t x;
-      if (q == 0) x = perm(1u, L[0], 0x04000102u);
-      else if (q <= 21) x = perm(L[q - 1], L[q], 0x07000102u);
-      else if (q == 22) x = perm(L[21], L[22], 0x0700010Cu) | (R[0] & 0xFFu);
-      else if (q <= 44) x = perm(R[q - 23], R[q - 22], 0x05060700u);
-      else if (q == 45) x = perm(R[22], 0x80u, 0x05000C0Cu);
-      else if (q == 47) x = 181u * 8u;
-      else x = 0u;
-      w[wi] = x;
-    }
+    for (int wi = 0; wi < 16; wi++) w[wi] = node_word(L, R, 16 * b + wi);
     sha256_compress(st, w);
   }
   bool rpar = (R[7] & 0xFFu) == 0xFFu;

@@ -55,14 +55,18 @@ __device__ __forceinline__ void sha_round(ShaRegs& r, uint32_t kw) {
   r.h = r.g; r.g = r.f; r.f = r.e; r.e = r.d + t1; r.d = r.c; r.c = r.b; r.b = r.a; r.a = t1 + t2;
 }
 
-// One compression of the 16-word block w (big-endian words) into st. Rounds run as
-// four unrolled 16-round bodies inside a rolled loop: the scheduler's window stays
-// one body wide, which keeps the state + 16-word window near 40 VGPRs instead of
-// letting it hoist the whole message schedule (200+ VGPRs, occupancy 2).
-__device__ __forceinline__ void sha256_compress(uint32_t (&st)[8], uint32_t (&w)[16]) {
-  ShaRegs r{st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7]};
+// Rounds [START, 64) of one compression of the 16-word block w into st, with r0 the
+// working variables after round START - 1. START > 0 skips the rounds of a message
+// prefix that is the same for every lane (precomputed by sha_midstate at compile time);
+// w must still hold the prefix words, the message schedule reads them. Rounds run as
+// four unrolled 16-round bodies inside a rolled loop: the scheduler's window stays one
+// body wide, which keeps the state + 16-word window near 40 VGPRs instead of letting it
+// hoist the whole message schedule (200+ VGPRs, occupancy 2).
+template <int START>
+__device__ __forceinline__ void sha256_compress_from(uint32_t (&st)[8], const ShaRegs& r0, uint32_t (&w)[16]) {
+  ShaRegs r = r0;
 #pragma unroll
-  for (int i = 0; i < 16; i++) sha_round(r, w[i] + kSha256K[i]);
+  for (int i = START; i < 16; i++) sha_round(r, w[i] + kSha256K[i]);
 #pragma unroll 1
   for (int base = 16; base < 64; base += 16) {
 #pragma unroll
@@ -77,6 +81,34 @@ __device__ __forceinline__ void sha256_compress(uint32_t (&st)[8], uint32_t (&w)
   }
   st[0] += r.a; st[1] += r.b; st[2] += r.c; st[3] += r.d;
   st[4] += r.e; st[5] += r.f; st[6] += r.g; st[7] += r.h;
+}
+
+__device__ __forceinline__ void sha256_compress(uint32_t (&st)[8], uint32_t (&w)[16]) {
+  sha256_compress_from<0>(st, ShaRegs{st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7]}, w);
+}
+
+// Compile-time SHA-256: working variables after the first n rounds of a first block
+// (chaining value = IV) whose words w[0..n) are constants. Used for the constant
+// prefixes of parity leaves (0x00 || 0xFF*27...) and parity inner nodes (0x01 || 0xFF*55).
+struct ShaMid {
+  uint32_t v[8];
+};
+constexpr uint32_t kShaKc[64] = {
+    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
+    0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u};
+constexpr uint32_t c_rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+constexpr ShaMid sha_midstate(const uint32_t* w, int n) {
+  uint32_t a = 0x6a09e667u, b = 0xbb67ae85u, c = 0x3c6ef372u, d = 0xa54ff53au;
+  uint32_t e = 0x510e527fu, f = 0x9b05688cu, g = 0x1f83d9abu, h = 0x5be0cd19u;
+  for (int i = 0; i < n; i++) {
+    const uint32_t t1 = h + (c_rotr(e, 6) ^ c_rotr(e, 11) ^ c_rotr(e, 25)) + ((e & f) ^ (~e & g)) + kShaKc[i] + w[i];
+    const uint32_t t2 = (c_rotr(a, 2) ^ c_rotr(a, 13) ^ c_rotr(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+  }
+  return ShaMid{{a, b, c, d, e, f, g, h}};
+}
+__device__ __forceinline__ ShaRegs mid_regs(const ShaMid& m) {
+  return ShaRegs{m.v[0], m.v[1], m.v[2], m.v[3], m.v[4], m.v[5], m.v[6], m.v[7]};
 }
 
 __device__ __forceinline__ void sha256_init(uint32_t (&st)[8]) {
