@@ -4,16 +4,18 @@
 set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
-out=gpurun_out/rschunk_hyb.txt
+out=gpurun_out/rs_ab_${VAR:-CEL_RS_CHUNK}.txt
 : > $out
-for c in 0 4 8 16 32 0; do
-  CEL_RS_CHUNK=$c timeout -k 10 120 python -u bench.py --no-cpu --k512-batch 0 > gpurun_out/rschunk_$c.log 2>&1
+VAR=${VAR:-CEL_RS_CHUNK}
+VALS=${VALS:-0 4 8 16 32 0}
+for c in $VALS; do
+  env $VAR=$c timeout -k 10 120 python -u bench.py --no-cpu --k512-batch 0 > gpurun_out/rschunk_$c.log 2>&1
   rc=$?; [ $rc -eq 0 ] || { echo "chunk $c rc=$rc" >> $out; exit $rc; }
-  python3 - "$c" >> $out <<'PY'
+  python3 - "$c" "$VAR" >> $out <<'PY'
 import json, sys
 c = sys.argv[1]
 d = json.loads(open(f"gpurun_out/rschunk_{c}.log").read().strip().splitlines()[-1])
-print(f"CEL_RS_CHUNK={c:>3s}: {d['value']:9.1f} squares/s  rs {d['roofline']['avg_launch_us'] / 256:6.2f} us/square"
+print(f"{sys.argv[2]}={c:>3s}: {d['value']:9.1f} squares/s  rs {d['roofline']['avg_launch_us'] / 256:6.2f} us/square"
       f" (frac {d['roofline']['frac']:.3f})  nmt {d['roofline_nmt']['avg_launch_us'] / 256:6.2f} us/square")
 PY
 done
