@@ -233,3 +233,25 @@ def test_device_batch(ctx, oracle, k, n, inplace):
     ctx.check(ctx.lib.cel_dev_extend_only(ctx.handle, d_ods, n, k, d_eds.ptr, None))
     synchronize()
     assert np.array_equal(d_eds.download((n, w, w, 512)), eds)
+
+
+@pytest.mark.parametrize("k,region", [(32, "quarter3"), (64, "quarter3"), (128, "quarter3"), (64, "all")])
+def test_parity_namespace_in_ods(ctx, oracle, k, region):
+    """ODS shares that carry the parity namespace 0xFF*29 themselves. Their subtrees
+    start with the same 0x01 || 0xFF*55 node prefix as Q1-Q3 subtrees, so the inner-node
+    midstate path (nmt_kernels.hip hash_node) runs on Q0 data too; the IgnoreMaxNamespace
+    rule (nmt hasher.go HashNode) applies to them by value. Rows and columns stay
+    namespace-ordered."""
+    ods = random_ods(k, 7000 + k)
+    if region == "all":
+        ods[:, :, :29] = 0xFF
+    else:  # every cell outside the top-left quarter of the ODS
+        h = k // 2
+        ods[h:, :, :29] = 0xFF
+        ods[:, h:, :29] = 0xFF
+    dev = run_device(ctx, ods)
+    eds, rr, cr, dah = oracle.extend_and_commit(ods)
+    assert np.array_equal(dev.cells, eds), "EDS bytes differ"
+    assert np.array_equal(dev._row_roots, rr), "row roots differ"
+    assert np.array_equal(dev._col_roots, cr), "column roots differ"
+    assert dev._dah == dah
