@@ -456,7 +456,9 @@ __global__ __launch_bounds__(64 * (1 << (LOGK - 5))) void k_rs_encode_gf16p(RsGe
       __builtin_amdgcn_sched_barrier(0);
     }
   }
-  // FFT, arrangement B
+  // FFT, arrangement B. The group at hb = 0 has skew index S*dh - 1 = 2^m - 1, whose
+  // skew is 0 (log = modulus: Leopard's FFT_DIT2 skips the multiply), so those
+  // butterflies are y ^= x only: the whole first layer and 1/2, 1/4, ... of the next.
 #pragma unroll
   for (int t = 0; (1 << t) < G; t++) {
     const int dh = G >> (t + 1);
@@ -469,7 +471,7 @@ __global__ __launch_bounds__(64 * (1 << (LOGK - 5))) void k_rs_encode_gf16p(RsGe
         for (int lo = 0; lo < L; lo++) {
           const int x = h * L + lo, y = (h + dh) * L + lo;
           pin2(wl[x], wh[x], wl[y], wh[y]);
-          gf16_muladd4(wl[x], wh[x], wl[y], wh[y], tb);
+          if (hb != 0) gf16_muladd4(wl[x], wh[x], wl[y], wh[y], tb);
           opaque(wl[x]);
           opaque(wh[x]);
           wl[y] ^= wl[x];
@@ -484,17 +486,18 @@ __global__ __launch_bounds__(64 * (1 << (LOGK - 5))) void k_rs_encode_gf16p(RsGe
   exchange(false);  // ends with a barrier: the image space is free again
   for (int i = lane; i < 31 * TW; i += 64) atab[i] = tw[(wv * S) * TW + i];  // FFT A: skew wv*S + m - 1
   __syncthreads();
-  // FFT, arrangement A
+  // FFT, arrangement A (wave 0, base 0: skew index D - 1 = 2^m - 1, multiply by zero)
 #pragma unroll
   for (int lg = LOGS - 1; lg >= 0; lg--) {
     const int D = 1 << lg;
 #pragma unroll
     for (int base = 0; base < S; base += 2 * D) {
       const Perm16 t = lds_tab16(atab + (base + D - 1) * TW);
+      const bool zero_tw = base == 0 && wv == 0;  // wave-uniform
 #pragma unroll
       for (int j = 0; j < D; j++) {
         pin2(wl[base + j], wh[base + j], wl[base + j + D], wh[base + j + D]);
-        gf16_muladd4(wl[base + j], wh[base + j], wl[base + j + D], wh[base + j + D], t);
+        if (!zero_tw) gf16_muladd4(wl[base + j], wh[base + j], wl[base + j + D], wh[base + j + D], t);
         opaque(wl[base + j]);
         opaque(wh[base + j]);
         wl[base + j + D] ^= wl[base + j];
