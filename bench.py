@@ -69,7 +69,7 @@ def parse():
                     help="eds: the upload places each ODS in Q0 of its EDS buffer and the extension "
                          "reads it in place; ods: separate contiguous ODS buffer, the row pass copies Q0")
     ap.add_argument("--phase-reps", type=int, default=10)
-    ap.add_argument("--k512-batch", type=int, default=8,
+    ap.add_argument("--k512-batch", type=int, default=32,
                     help="with --k 128: k=512 squares per step per GPU of the companion line (0 = off)")
     ap.add_argument("--k512-steps", type=int, default=5)
     ap.add_argument("--mode", default="batch", choices=["batch", "sharded", "repair"],
