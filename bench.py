@@ -12,6 +12,8 @@ Besides the headline number the JSON line carries:
                 square / measured average duration (HIP events on the launch stream)
   roofline_nmt  NMT+DAH phase: SHA-256 compressions (60 k^2 + 4k - 2 per square)
                 per second vs the integer-VALU issue peak
+  k512          (default --k 128 run) the same measurement on a short batch of k=512
+                squares (GF(2^16)), since the metric names k=128 and k=512
   cpu_baseline  the C restatement (oracle/, SIMD + OpenMP) on a bounded sample of the
                 same squares, rank 0 at N = 1 only; its DAHs also cross-check the GPU
 """
