@@ -294,6 +294,12 @@ struct Perm16 {
   uint32_t t[kTw16Words];
 };
 
+// Cache policy of the data loads and stores (2 = nt: every byte is touched once per pass).
+#ifndef CEL_GF16_CP
+#define CEL_GF16_CP 2
+#endif
+constexpr int kGf16Cp = CEL_GF16_CP;
+
 // One product table from LDS (wave-uniform address: a broadcast read, ~LDS latency instead
 // of an L2 round trip per twiddle group).
 __device__ __forceinline__ Perm16 lds_tab16(const uint32_t* p) {
@@ -373,8 +379,8 @@ __global__ __launch_bounds__(64 * (1 << (LOGK - 5))) void k_rs_encode_gf16p(RsGe
 #pragma unroll
   for (int i = 0; i < S; i++) {
     const uint32_t so = (uint32_t)(wv * S + i) * in_shard;
-    wl[i] = __builtin_amdgcn_raw_buffer_load_b32(rin, col, so, 0);
-    wh[i] = __builtin_amdgcn_raw_buffer_load_b32(rin, col + 32, so, 0);
+    wl[i] = __builtin_amdgcn_raw_buffer_load_b32(rin, col, so, kGf16Cp);
+    wh[i] = __builtin_amdgcn_raw_buffer_load_b32(rin, col + 32, so, kGf16Cp);
   }
   // shard j -> byte offset, linear or blocked (see RsGeom::blk_log)
   const uint32_t blk_mask = g.blk_log ? (1u << g.blk_log) - 1u : 0xFFFFFFFFu;
@@ -515,8 +521,8 @@ __global__ __launch_bounds__(64 * (1 << (LOGK - 5))) void k_rs_encode_gf16p(RsGe
 #pragma unroll
   for (int i = 0; i < S; i++) {
     const uint32_t so = place((uint32_t)(wv * S + i), out_shard, out_blk);
-    __builtin_amdgcn_raw_buffer_store_b32(wl[i], rout, col, so, 0);
-    __builtin_amdgcn_raw_buffer_store_b32(wh[i], rout, col + 32, so, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(wl[i], rout, col, so, kGf16Cp);
+    __builtin_amdgcn_raw_buffer_store_b32(wh[i], rout, col + 32, so, kGf16Cp);
   }
 }
 
