@@ -247,7 +247,7 @@ def run_repair(a):
             torch.cuda.current_stream().synchronize()
             pres = present.copy()
             ctx.check(ctx.lib.cel_dev_repair(ctx.handle, ctypes.c_void_p(d_work.data_ptr()), P(pres), k, P(rra),
-                                             P(cra), None, None))
+                                             P(cra), None, None, None, None))
             return d_work
 
     for _ in range(a.warmup):

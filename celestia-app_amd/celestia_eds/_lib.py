@@ -14,7 +14,7 @@ _ROOT = os.path.dirname(_PKG_DIR)
 LIB_PATH = os.environ.get("CEL_EDS_LIB", os.path.join(_ROOT, "libcelestia_eds.so"))
 
 OK, EINVAL, ENOTPOW2, ECHUNK, ETOOBIG, EORDER, ETOOFEW, EBYZANTINE, EUNREPAIRABLE, EDEVICE, ENOMEM, \
-    ESHORT, EPUSHPAST = range(13)
+    ESHORT, EPUSHPAST, EBADROOT = range(14)
 FLAG_ORDER_CHECK = 0x1
 SHARE_SIZE = 512
 NAMESPACE_SIZE = 29
@@ -76,8 +76,8 @@ def load():
             "cel_axis_root": (i32, [P, P, u32, u32, u32, P, u32]),
             "cel_nmt_root": (i32, [P, P, u32, u32, P, u32]),
             "cel_dah_hash": (i32, [P, P, P, u32, P]),
-            "cel_repair": (i32, [P, P, P, u32, u32, P, P, P, P]),
-            "cel_dev_repair": (i32, [P, P, P, u32, P, P, P, P]),
+            "cel_repair": (i32, [P, P, P, u32, u32, P, P, P, P, P, P]),
+            "cel_dev_repair": (i32, [P, P, P, u32, P, P, P, P, P, P]),
             "cel_dev_shard_workspace_size": (sz, [u32, u32]),
             "cel_dev_shard_rows": (i32, [P, P, u32, u32, P, P]),
             "cel_dev_shard_cols": (i32, [P, P, u32, u32, u32, P, P, P, P, P, u32]),

@@ -69,6 +69,10 @@ def NewErasuredNamespacedMerkleTree(square_size, axis_index):
 
 
 def NewConstructor(square_size):
+    """wrapper.NewConstructor (nmt_wrapper.go:73-86). Marked as the default constructor:
+    rsmt2d.ComputeExtendedDataSquare serves it with the device pass's roots."""
     def NewTree(_axis, axis_index):
         return ErasuredNamespacedMerkleTree(square_size, axis_index)
+    NewTree._cel_wrapper_constructor = True
+    NewTree.square_size = square_size
     return NewTree

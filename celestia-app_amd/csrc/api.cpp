@@ -149,6 +149,7 @@ const char* cel_strerror(cel_status st) {
     case CEL_ENOMEM: return "device out of memory";
     case CEL_ESHORT: return "data is too short to contain namespace ID";
     case CEL_EPUSHPAST: return "pushed past predetermined square size";
+    case CEL_EBADROOT: return "bad root input";
     default: return "unknown status";
   }
 }
@@ -241,6 +242,7 @@ static hipError_t place_ods(const void* src, uint32_t n, uint32_t k, void* d_eds
 
 cel_status cel_dev_place_ods(cel_ctx* ctx, const void* ods, uint32_t n, uint32_t k, void* d_eds, void* stream) {
   if (!ctx || !ods || !d_eds || !n) return CEL_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
   cel_status st = validate_square(ctx, k, kShare);
   if (st) return st;
   DeviceGuard g(ctx->device);
@@ -250,6 +252,7 @@ cel_status cel_dev_place_ods(cel_ctx* ctx, const void* ods, uint32_t n, uint32_t
 
 cel_status cel_dev_extend_only(cel_ctx* ctx, const void* d_ods, uint32_t n, uint32_t k, void* d_eds, void* stream) {
   if (!ctx || !d_eds || !n) return CEL_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
   cel_status st = validate_square(ctx, k, kShare);
   if (st) return st;
   DeviceGuard g(ctx->device);
@@ -267,6 +270,7 @@ cel_status cel_dev_commit_only(cel_ctx* ctx, const void* d_eds, uint32_t n, uint
                                void* d_col_roots, void* d_dah, int32_t* d_status, void* d_work, void* stream,
                                uint32_t flags) {
   if (!ctx || !d_eds || !n || !d_row_roots || !d_col_roots || !d_dah || !d_work) return CEL_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
   cel_status st = validate_square(ctx, k, kShare);
   if (st) return st;
   DeviceGuard g(ctx->device);
@@ -280,6 +284,7 @@ cel_status cel_dev_extend_batch(cel_ctx* ctx, const void* d_ods, uint32_t n, uin
                                 void* d_row_roots, void* d_col_roots, void* d_dah, int32_t* d_status, void* d_work,
                                 void* stream, uint32_t flags) {
   if (!ctx || !d_eds || !n || !d_row_roots || !d_col_roots || !d_dah || !d_work) return CEL_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
   cel_status st = validate_square(ctx, k, kShare);
   if (st) return st;
   DeviceGuard g(ctx->device);
@@ -420,6 +425,7 @@ size_t cel_dev_shard_workspace_size(uint32_t k, uint32_t nranks) {
 cel_status cel_dev_shard_rows(cel_ctx* ctx, const void* d_ods_rows, uint32_t k, uint32_t nranks, void* d_send,
                               void* stream) {
   if (!ctx || !d_ods_rows || !d_send) return CEL_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
   cel_status st = validate_shard(ctx, k, nranks);
   if (st) return st;
   DeviceGuard g(ctx->device);
@@ -457,6 +463,7 @@ cel_status cel_dev_shard_cols(cel_ctx* ctx, void* d_slab, uint32_t k, uint32_t n
                               void* d_col_rec, void* d_row_sub, int32_t* d_status, void* d_work, void* stream,
                               uint32_t flags) {
   if (!ctx || !d_slab || !d_col_rec || !d_row_sub || !d_status || !d_work) return CEL_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
   cel_status st = validate_shard(ctx, k, nranks);
   if (st) return st;
   if (rank >= nranks) return fail(ctx, CEL_EINVAL, "rank out of range");
@@ -489,6 +496,7 @@ cel_status cel_dev_shard_finish(cel_ctx* ctx, const void* d_row_sub_all, const v
                                 int32_t* d_status, void* d_work, void* stream, uint32_t flags) {
   if (!ctx || !d_row_sub_all || !d_col_rec_all || !d_row_roots || !d_col_roots || !d_dah || !d_status || !d_work)
     return CEL_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
   cel_status st = validate_shard(ctx, k, nranks);
   if (st) return st;
   DeviceGuard g(ctx->device);
@@ -504,9 +512,8 @@ cel_status cel_dev_shard_finish(cel_ctx* ctx, const void* d_row_sub_all, const v
 
 uint64_t cel_codec_max_chunks(void) { return 32768ull * 32768ull; }
 const char* cel_codec_name(void) { return "Leopard"; }
-cel_status cel_codec_validate_chunk_size(uint32_t len) {
-  return (len == 0 || (len % 64) != 0) ? CEL_ECHUNK : CEL_OK;
-}
+// rsmt2d LeoRSCodec.ValidateChunkSize: chunkSize % 64 == 0 (zero passes).
+cel_status cel_codec_validate_chunk_size(uint32_t len) { return (len % 64) != 0 ? CEL_ECHUNK : CEL_OK; }
 
 cel_status cel_codec_encode(cel_ctx* ctx, const uint8_t* data, uint32_t n, uint32_t len, uint8_t* parity) {
   if (!ctx) return CEL_EINVAL;
@@ -515,6 +522,7 @@ cel_status cel_codec_encode(cel_ctx* ctx, const uint8_t* data, uint32_t n, uint3
   if (cel_codec_validate_chunk_size(len)) return fail(ctx, CEL_ECHUNK, "shard size must be a multiple of 64");
   if (!is_pow2(n)) return fail(ctx, CEL_ENOTPOW2, "number of data shards is not a power of 2");
   if (n > kMaxGf16Width) return fail(ctx, CEL_ETOOBIG, "too many shards for the device path");
+  if (len == 0) return CEL_OK;  // empty shards: empty parity
   DeviceGuard g(ctx->device);
   hipError_t e = hipSuccess;
   const size_t b = (size_t)n * len;
@@ -550,6 +558,7 @@ cel_status cel_codec_decode(cel_ctx* ctx, uint8_t* shards, const uint8_t* presen
   for (uint32_t i = 0; i < 2 * n; i++) have += present[i] ? 1 : 0;
   if (have == 2 * n) return CEL_OK;
   if (have < n) return fail(ctx, CEL_ETOOFEW, "too few shards given");
+  if (len == 0) return CEL_OK;
   DeviceGuard g(ctx->device);
   hipError_t e = hipSuccess;
   const size_t b = (size_t)2 * n * len;
@@ -781,9 +790,10 @@ cel_status cel_get_commitment(cel_ctx* ctx, const uint8_t* eds, uint32_t k, uint
 
 // ------------------------------------------------------------------- repair
 
-// rsmt2d Repair crossword loop. The control loop (which axes are solvable) runs
-// on the host over the presence mask; decoding, re-encoding, byte comparisons and
-// root computation run on the device over the EDS kept resident.
+// rsmt2d v0.14.0 ExtendedDataSquare.Repair [dep] (extendeddatacrossword.go), with the
+// oracle's restatement (oracle/eds.c) as the checker. The crossword control loop runs on
+// the host over the presence mask; decoding, re-encoding, byte comparisons and root
+// computation run on the device over the EDS kept resident.
 namespace {
 
 struct RepairBufs {
@@ -793,23 +803,26 @@ struct RepairBufs {
   uint8_t* dmask;
   uint8_t* tmp;
   int32_t* idx;
-  int32_t* flags;  // [2][W] encoding-check flags by (direction, axis)
+  int32_t* flags;  // [2][W] encoding-check flags by (direction, axis): an axis completes once
 };
 
-// One crossword pass over `list` (axes of one direction with >= k known cells):
-// decode them, re-encode the data half and compare it with the decoded parity half
-// (rsmt2d verifyEncoding); mismatches set flags_all[is_col*W + axis]. Nothing is
-// synchronised: every check result is read back once at the end of the repair.
-static cel_status solve_pass(cel_ctx* ctx, const RepairBufs& b, uint32_t k, int is_col,
-                             const std::vector<int32_t>& list) {
+// Re-encode check of `list` (axes of one direction): the data half of each axis is
+// encoded again and compared with its parity half; mismatches set flags[is_col*W + axis].
+// decode: the axes are incomplete and get decoded first (rsmt2d solveCrossword) and the
+// decoded cells are scattered back into the square; otherwise they are complete already
+// (preRepairSanityCheck, and the orthogonal axes a solve completes). Nothing is
+// synchronised: every flag is read back once at the end of the repair.
+static cel_status axes_pass(cel_ctx* ctx, const RepairBufs& b, uint32_t k, int is_col,
+                            const std::vector<int32_t>& list, bool decode) {
   const uint32_t W = 2 * k, na = (uint32_t)list.size();
+  if (!na) return CEL_OK;
   hipStream_t s = ctx->stream;
   hipError_t e;
   if ((e = hipMemcpyAsync(b.idx, list.data(), na * 4, hipMemcpyHostToDevice, s)) != hipSuccess)
     return hip_fail(ctx, e, "H2D");
   if ((e = launch_gather_axes(b.eds, b.mask, W, b.idx, is_col, na, b.dense, b.dmask, s)) != hipSuccess)
     return hip_fail(ctx, e, "gather");
-  if ((e = launch_rs_decode(b.dense, b.dmask, na, k, kShare, ctx->tables, nullptr, s)) != hipSuccess)
+  if (decode && (e = launch_rs_decode(b.dense, b.dmask, na, k, kShare, ctx->tables, nullptr, s)) != hipSuccess)
     return hip_fail(ctx, e, "decode");
   RsGeom g{};
   g.in = b.dense;
@@ -828,23 +841,43 @@ static cel_status solve_pass(cel_ctx* ctx, const RepairBufs& b, uint32_t k, int 
   if ((e = launch_cmp(b.tmp, (uint64_t)k * kShare, b.dense + (uint64_t)k * kShare, (uint64_t)W * kShare,
                       (uint64_t)k * kShare, na, b.flags + (size_t)is_col * W, s, b.idx)) != hipSuccess)
     return hip_fail(ctx, e, "compare");
-  if ((e = launch_scatter_axes(b.eds, b.mask, W, b.idx, is_col, na, b.dense, s)) != hipSuccess)
+  if (decode && (e = launch_scatter_axes(b.eds, b.mask, W, b.idx, is_col, na, b.dense, s)) != hipSuccess)
     return hip_fail(ctx, e, "scatter");
-  // the next pass rewrites b.idx: the stream orders it after this pass's kernels, and
-  // the host list is read before hipMemcpyAsync returns (pageable source)
+  // the next pass rewrites b.idx after these kernels (stream order); `list` stays alive
+  // in the caller until the final synchronisation
   return CEL_OK;
 }
 
-// rsmt2d Repair over the EDS resident at b.eds. hm = host presence mask (updated).
-// The crossword control loop runs on the host over the mask; no pass waits for the
-// device. Root checks are deferred: an axis, once complete, never changes, so one
-// commit pass over the final square gives every root rsmt2d checks along the way, and
-// the checks are replayed in rsmt2d's order (prerepairSanityCheck rows then columns,
-// then each solved axis in pass order, encoding check before root check, then the
-// final all-axes verification), reporting the same first failing axis.
+// One check of the replay, in rsmt2d's order (oracle/eds.c orc_repair):
+//   SANITY  an axis complete before the repair: root (else "bad root input"), encoding
+//   SOLVE   an axis decoded by solve `solve`: encoding, root
+//   ORTH    an axis that solve `solve` completed: root, encoding
+struct Check {
+  enum Kind { SANITY, SOLVE, ORTH } kind;
+  int is_col;
+  int32_t idx;
+  int32_t solve;  // index into the solve log (-1 for SANITY)
+};
+struct Solve {
+  int is_col;
+  int32_t idx;
+  std::vector<uint8_t> before;  // the axis's presence mask before the solve
+};
+
+struct RepairOut {
+  int32_t* bad_axis;
+  int32_t* bad_index;
+  uint8_t* byz_shares;   // nullable, W * 512
+  uint8_t* byz_present;  // nullable, W
+};
+
+// rsmt2d Repair over the EDS resident at b.eds. hm = host presence mask (updated: all
+// ones on success, the mask before the failing solve on a byzantine / bad-root error).
+// No pass waits for the device. Root checks are deferred: an axis, once complete, never
+// changes, so one commit pass over the final square gives every root rsmt2d checks on
+// the way, and the checks are replayed in rsmt2d's order, reporting the first failure.
 static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>& hm, uint32_t k,
-                              const uint8_t* row_roots, const uint8_t* col_roots, int32_t* bad_axis,
-                              int32_t* bad_index) {
+                              const uint8_t* row_roots, const uint8_t* col_roots, const RepairOut& out) {
   const uint32_t W = 2 * k;
   const size_t cells = (size_t)W * W;
   hipStream_t s = ctx->stream;
@@ -853,42 +886,65 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
   if ((e = hipMemcpyAsync(b.mask, hm.data(), cells, hipMemcpyHostToDevice, s)) != hipSuccess ||
       (e = hipMemsetAsync(b.flags, 0, 2 * (size_t)W * 4, s)) != hipSuccess)
     return hip_fail(ctx, e, "H2D");
+  const std::vector<uint8_t> initial = hm;
+  auto at = [&](int is_col, uint32_t i, uint32_t j) -> uint8_t& {
+    return is_col ? hm[(size_t)j * W + i] : hm[(size_t)i * W + j];
+  };
   auto count = [&](int is_col, uint32_t i) {
     uint32_t c = 0;
-    for (uint32_t j = 0; j < W; j++) c += is_col ? hm[(size_t)j * W + i] : hm[(size_t)i * W + j];
+    for (uint32_t j = 0; j < W; j++) c += at(is_col, i, j);
     return c;
   };
-  struct Check {
-    int is_col;
-    int32_t idx;
-    bool solved;  // also has an encoding-check flag
-  };
   std::vector<Check> order;
-  // prerepairSanityCheck: complete axes must match their roots.
-  for (int is_col = 0; is_col < 2; is_col++)
-    for (uint32_t i = 0; i < W; i++)
-      if (count(is_col, i) == W) order.push_back({is_col, (int32_t)i, false});
-  // crossword: alternate rows and columns until solved or stuck
+  std::vector<Solve> solves;
   std::vector<std::vector<int32_t>> lists;  // kept alive until the final sync
+  // preRepairSanityCheck: for i: row i, column i
+  {
+    std::vector<int32_t> comp[2];
+    for (uint32_t i = 0; i < W; i++)
+      for (int is_col = 0; is_col < 2; is_col++)
+        if (count(is_col, i) == W) {
+          order.push_back({Check::SANITY, is_col, (int32_t)i, -1});
+          comp[is_col].push_back((int32_t)i);
+        }
+    for (int is_col = 0; is_col < 2; is_col++) {
+      if ((st = axes_pass(ctx, b, k, is_col, comp[is_col], false)) != CEL_OK) return st;
+      lists.push_back(std::move(comp[is_col]));
+    }
+  }
+  // solveCrossword: all rows, then all columns, until solved or stuck
   bool solved = false;
   for (;;) {
     bool progress = false;
     for (int is_col = 0; is_col < 2; is_col++) {
-      std::vector<int32_t> list;
+      std::vector<int32_t> list, orth;
       for (uint32_t i = 0; i < W; i++) {
         const uint32_t c = count(is_col, i);
         if (c >= k && c < W) list.push_back((int32_t)i);
       }
       if (list.empty()) continue;
-      if ((st = solve_pass(ctx, b, k, is_col, list)) != CEL_OK) return st;
+      if ((st = axes_pass(ctx, b, k, is_col, list, true)) != CEL_OK) return st;
+      // sequential view of the pass: solve i fills its missing cells, completing the
+      // orthogonal axes whose only missing cell it was
       for (int32_t i : list) {
-        order.push_back({is_col, i, true});
+        Solve sv{is_col, i, std::vector<uint8_t>(W)};
+        for (uint32_t j = 0; j < W; j++) sv.before[j] = at(is_col, (uint32_t)i, j);
+        const int32_t si = (int32_t)solves.size();
+        order.push_back({Check::SOLVE, is_col, i, si});
         for (uint32_t j = 0; j < W; j++) {
-          if (is_col) hm[(size_t)j * W + i] = 1;
-          else hm[(size_t)i * W + j] = 1;
+          if (sv.before[j]) continue;
+          at(is_col, (uint32_t)i, j) = 1;
+          if (count(!is_col, j) == W) {
+            order.push_back({Check::ORTH, !is_col, (int32_t)j, si});
+            orth.push_back((int32_t)j);
+          }
         }
+        solves.push_back(std::move(sv));
       }
+      std::sort(orth.begin(), orth.end());
+      if ((st = axes_pass(ctx, b, k, !is_col, orth, false)) != CEL_OK) return st;
       lists.push_back(std::move(list));
+      lists.push_back(std::move(orth));
       progress = true;
     }
     size_t have = 0;
@@ -901,7 +957,7 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
   }
   // every root of the (possibly partial) square in one commit pass, roots only
   const size_t roots_b = (size_t)W * kNode;
-  uint8_t* d_rr = b.tmp;  // free after the last solve pass (stream order)
+  uint8_t* d_rr = b.tmp;  // free after the last pass (stream order)
   uint8_t* d_cr = b.tmp + roots_b;
   if ((e = launch_commit(b.eds, k, 1, d_rr, d_cr, nullptr, nullptr, b.dense, false, s)) != hipSuccess)
     return hip_fail(ctx, e, "roots");
@@ -915,19 +971,66 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
     const uint8_t* exp = (is_col ? col_roots : row_roots) + (size_t)i * kNode;
     return std::memcmp(got.data() + is_col * roots_b + (size_t)i * kNode, exp, kNode) == 0;
   };
-  auto byz = [&](int is_col, int32_t idx) {
-    if (bad_axis) *bad_axis = is_col;
-    if (bad_index) *bad_index = idx;
-    return fail(ctx, CEL_EBYZANTINE, std::string("byzantine ") + (is_col ? "column" : "row") + " " +
-                                         std::to_string(idx));
+  auto enc_ok = [&](int is_col, int32_t i) { return flags[(size_t)is_col * W + i] == 0; };
+  // the presence mask before solve `upto` (all solves before it applied)
+  auto rollback = [&](int32_t upto) {
+    hm = initial;
+    for (int32_t t = 0; t < upto; t++)
+      for (uint32_t j = 0; j < W; j++) at(solves[t].is_col, (uint32_t)solves[t].idx, j) = 1;
   };
-  for (const Check& c : order)
-    if ((c.solved && flags[(size_t)c.is_col * W + c.idx]) || !root_ok(c.is_col, c.idx)) return byz(c.is_col, c.idx);
+  auto fail_axis = [&](cel_status code, int is_col, int32_t idx, const uint8_t* axis_mask) {
+    if (out.bad_axis) *out.bad_axis = is_col;
+    if (out.bad_index) *out.bad_index = idx;
+    if (code == CEL_EBYZANTINE && (out.byz_shares || out.byz_present)) {
+      // ErrByzantineData.Shares: the axis's cells from the square (complete axes never
+      // change; cells of a solved axis present before its solve kept their bytes)
+      std::vector<uint8_t> axis((size_t)W * kShare);
+      const uint8_t* src = b.eds + (is_col ? (size_t)idx * kShare : (size_t)idx * W * kShare);
+      const hipError_t ce = is_col ? hipMemcpy2D(axis.data(), kShare, src, (size_t)W * kShare, kShare, W,
+                                                  hipMemcpyDeviceToHost)
+                                   : hipMemcpy(axis.data(), src, axis.size(), hipMemcpyDeviceToHost);
+      if (ce != hipSuccess) return hip_fail(ctx, ce, "byzantine shares");
+      for (uint32_t j = 0; j < W; j++) {
+        const uint8_t p = axis_mask ? axis_mask[j] : 1;
+        if (out.byz_present) out.byz_present[j] = p;
+        if (out.byz_shares) {
+          if (p) std::memcpy(out.byz_shares + (size_t)j * kShare, axis.data() + (size_t)j * kShare, kShare);
+          else std::memset(out.byz_shares + (size_t)j * kShare, 0, kShare);
+        }
+      }
+    }
+    const char* dir = is_col ? "col" : "row";
+    return fail(ctx, code, code == CEL_EBADROOT
+                               ? std::string("bad root input: ") + dir + " " + std::to_string(idx)
+                               : std::string("byzantine ") + (is_col ? "column" : "row") + " " + std::to_string(idx));
+  };
+  for (const Check& c : order) {
+    switch (c.kind) {
+      case Check::SANITY:
+        if (!root_ok(c.is_col, c.idx)) {
+          rollback(0);
+          return fail_axis(CEL_EBADROOT, c.is_col, c.idx, nullptr);
+        }
+        if (!enc_ok(c.is_col, c.idx)) {
+          rollback(0);
+          return fail_axis(CEL_EBYZANTINE, c.is_col, c.idx, nullptr);
+        }
+        break;
+      case Check::SOLVE:
+        if (!enc_ok(c.is_col, c.idx) || !root_ok(c.is_col, c.idx)) {
+          rollback(c.solve);
+          return fail_axis(CEL_EBYZANTINE, c.is_col, c.idx, solves[c.solve].before.data());
+        }
+        break;
+      case Check::ORTH:
+        if (!root_ok(c.is_col, c.idx) || !enc_ok(c.is_col, c.idx)) {
+          rollback(c.solve);
+          return fail_axis(CEL_EBYZANTINE, c.is_col, c.idx, nullptr);
+        }
+        break;
+    }
+  }
   if (!solved) return fail(ctx, CEL_EUNREPAIRABLE, "failed to solve data square");
-  // Every axis solved along one direction must also match on the other.
-  for (int is_col = 0; is_col < 2; is_col++)
-    for (uint32_t i = 0; i < W; i++)
-      if (!root_ok(is_col, (int32_t)i)) return byz(is_col, (int32_t)i);
   return CEL_OK;
 }
 
@@ -954,7 +1057,8 @@ static cel_status repair_bufs(cel_ctx* ctx, uint32_t k, bool own_eds, RepairBufs
 
 
 cel_status cel_repair(cel_ctx* ctx, uint8_t* eds, uint8_t* present, uint32_t k, uint32_t share_size,
-                      const uint8_t* row_roots, const uint8_t* col_roots, int32_t* bad_axis, int32_t* bad_index) {
+                      const uint8_t* row_roots, const uint8_t* col_roots, int32_t* bad_axis, int32_t* bad_index,
+                      uint8_t* byz_shares, uint8_t* byz_present) {
   if (!ctx) return CEL_EINVAL;
   std::lock_guard<std::mutex> lock(ctx->mu);
   if (!eds || !present || !row_roots || !col_roots) return fail(ctx, CEL_EINVAL, "nil argument");
@@ -972,15 +1076,18 @@ cel_status cel_repair(cel_ctx* ctx, uint8_t* eds, uint8_t* present, uint32_t k, 
   std::vector<uint8_t> hm(cells);
   for (size_t i = 0; i < cells; i++) hm[i] = present[i] ? 1 : 0;
   if ((e = hipMemcpyAsync(b.eds, eds, eds_b, hipMemcpyHostToDevice, s)) != hipSuccess) return hip_fail(ctx, e, "H2D");
-  if ((st = repair_core(ctx, b, hm, k, row_roots, col_roots, bad_axis, bad_index)) != CEL_OK) return st;
+  st = repair_core(ctx, b, hm, k, row_roots, col_roots, RepairOut{bad_axis, bad_index, byz_shares, byz_present});
+  if (st != CEL_OK && st != CEL_EBYZANTINE && st != CEL_EBADROOT && st != CEL_EUNREPAIRABLE) return st;
+  // the (partially) repaired square goes back either way, with the mask it is valid under
   if ((e = hipMemcpyAsync(eds, b.eds, eds_b, hipMemcpyDeviceToHost, s)) != hipSuccess) return hip_fail(ctx, e, "D2H");
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "sync");
-  for (size_t i = 0; i < cells; i++) present[i] = 1;
-  return CEL_OK;
+  std::memcpy(present, hm.data(), cells);
+  return st;
 }
 
 cel_status cel_dev_repair(cel_ctx* ctx, void* d_eds, uint8_t* present, uint32_t k, const uint8_t* row_roots,
-                          const uint8_t* col_roots, int32_t* bad_axis, int32_t* bad_index) {
+                          const uint8_t* col_roots, int32_t* bad_axis, int32_t* bad_index, uint8_t* byz_shares,
+                          uint8_t* byz_present) {
   if (!ctx) return CEL_EINVAL;
   std::lock_guard<std::mutex> lock(ctx->mu);
   if (!d_eds || !present || !row_roots || !col_roots) return fail(ctx, CEL_EINVAL, "nil argument");
@@ -995,9 +1102,10 @@ cel_status cel_dev_repair(cel_ctx* ctx, void* d_eds, uint8_t* present, uint32_t 
   if ((st = repair_bufs(ctx, k, false, &b)) != CEL_OK) return st;
   std::vector<uint8_t> hm(cells);
   for (size_t i = 0; i < cells; i++) hm[i] = present[i] ? 1 : 0;
-  if ((st = repair_core(ctx, b, hm, k, row_roots, col_roots, bad_axis, bad_index)) != CEL_OK) return st;
-  for (size_t i = 0; i < cells; i++) present[i] = 1;
-  return CEL_OK;
+  st = repair_core(ctx, b, hm, k, row_roots, col_roots, RepairOut{bad_axis, bad_index, byz_shares, byz_present});
+  if (st == CEL_OK || st == CEL_EBYZANTINE || st == CEL_EBADROOT || st == CEL_EUNREPAIRABLE)
+    std::memcpy(present, hm.data(), cells);
+  return st;
 }
 
 }  // extern "C"

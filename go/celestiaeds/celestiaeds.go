@@ -1,12 +1,16 @@
 // Package celestiaeds binds libcelestia_eds.so (MI355X / gfx950) behind the
-// reference's own Go surface. It is a sketch of the cgo stub a celestia-app
-// maintainer would add; this repository's build image has no Go toolchain, so it
-// is not compiled or tested here (parity is established through the C ABI tests).
+// reference's own Go surface: rsmt2d's Codec, TreeConstructorFn / Tree and
+// ErrByzantineData types (rsmt2d v0.14.0, go.mod:13). It is the cgo stub a
+// celestia-app maintainer would add as pkg/celestiaeds of module
+// github.com/celestiaorg/celestia-app/v3; this repository's build image has no Go
+// toolchain, so it is not compiled here (parity is established through the C ABI
+// tests, which drive the same entry points).
 //
 // Replaces, without changing signatures:
-//   pkg/da/data_availability_header.go:65  da.ExtendShares
-//   pkg/da/data_availability_header.go:44  da.NewDataAvailabilityHeader (roots precomputed)
-//   pkg/appconsts/global_consts.go:92       appconsts.DefaultCodec (rsmt2d.Codec)
+//   pkg/da/data_availability_header.go:65  da.ExtendShares (ExtendSquare below)
+//   pkg/da/data_availability_header.go:44  da.NewDataAvailabilityHeader (roots precomputed, RootTable)
+//   pkg/appconsts/global_consts.go:92       appconsts.DefaultCodec (Codec, an rsmt2d.Codec)
+//   rsmt2d ExtendedDataSquare.Repair        (Context.Repair, used by celestia-node)
 package celestiaeds
 
 /*
@@ -22,6 +26,8 @@ import (
 	"fmt"
 	"sync"
 	"unsafe"
+
+	"github.com/celestiaorg/rsmt2d"
 )
 
 const (
@@ -30,12 +36,10 @@ const (
 	flagOrder    = C.CEL_FLAG_ORDER_CHECK
 )
 
-// Status codes map 1:1 onto the reference's Go errors (include/celestia_eds.h).
-var (
-	ErrNotPow2       = errors.New("number of shares is not a power of 2")
-	ErrByzantineData = errors.New("byzantine data")
-	ErrUnrepairable  = errors.New("failed to solve data square")
-)
+// Status codes map onto the reference's Go errors (include/celestia_eds.h):
+// CEL_EBYZANTINE -> *rsmt2d.ErrByzantineData, CEL_EUNREPAIRABLE ->
+// rsmt2d.ErrUnrepairableDataSquare, the rest -> errors carrying the reference's message.
+var ErrNotPow2 = errors.New("number of shares is not a power of 2")
 
 type Context struct {
 	mu  sync.Mutex
@@ -52,7 +56,16 @@ func NewContext(device int) (*Context, error) {
 
 func (c *Context) Close() { C.cel_ctx_destroy(c.ctx) }
 
-func (c *Context) err(st C.cel_status) error {
+// call runs f (a cel_* call on c.ctx) under c.mu and turns its status into an error,
+// reading cel_last_error before the lock is released (another goroutine's call on the
+// same ctx would overwrite it).
+func (c *Context) call(f func() C.cel_status) error {
+	c.mu.Lock()
+	defer c.mu.Unlock()
+	return c.errLocked(f())
+}
+
+func (c *Context) errLocked(st C.cel_status) error {
 	if st == C.CEL_OK {
 		return nil
 	}
@@ -60,10 +73,8 @@ func (c *Context) err(st C.cel_status) error {
 	switch st {
 	case C.CEL_ENOTPOW2:
 		return fmt.Errorf("%w: %s", ErrNotPow2, msg)
-	case C.CEL_EBYZANTINE:
-		return fmt.Errorf("%w: %s", ErrByzantineData, msg)
 	case C.CEL_EUNREPAIRABLE:
-		return ErrUnrepairable
+		return rsmt2d.ErrUnrepairableDataSquare
 	}
 	return errors.New(msg)
 }
@@ -90,12 +101,12 @@ func (c *Context) ExtendShares(shares [][]byte) (flat []byte, rowRoots, colRoots
 	rr := make([]byte, w*NmtNodeSize)
 	cr := make([]byte, w*NmtNodeSize)
 	dah = make([]byte, 32)
-	c.mu.Lock()
-	st := C.cel_extend_shares(c.ctx, (*C.uint8_t)(buf), C.uint32_t(n), ShareSize,
-		(*C.uint8_t)(unsafe.Pointer(&flat[0])), (*C.uint8_t)(unsafe.Pointer(&rr[0])),
-		(*C.uint8_t)(unsafe.Pointer(&cr[0])), (*C.uint8_t)(unsafe.Pointer(&dah[0])), flagOrder)
-	c.mu.Unlock()
-	if err = c.err(st); err != nil {
+	err = c.call(func() C.cel_status {
+		return C.cel_extend_shares(c.ctx, (*C.uint8_t)(buf), C.uint32_t(n), ShareSize,
+			(*C.uint8_t)(unsafe.Pointer(&flat[0])), (*C.uint8_t)(unsafe.Pointer(&rr[0])),
+			(*C.uint8_t)(unsafe.Pointer(&cr[0])), (*C.uint8_t)(unsafe.Pointer(&dah[0])), flagOrder)
+	})
+	if err != nil {
 		return nil, nil, nil, nil, err
 	}
 	for i := 0; i < w; i++ {
@@ -105,10 +116,33 @@ func (c *Context) ExtendShares(shares [][]byte) (flat []byte, rowRoots, colRoots
 	return flat, rowRoots, colRoots, dah, nil
 }
 
+// ExtendSquare is da.ExtendShares on the device (data_availability_header.go:65-75):
+// the same power-of-two check and error, then one device pass, and an
+// *rsmt2d.ExtendedDataSquare imported with a RootTable constructor, so
+// da.NewDataAvailabilityHeader's eds.RowRoots()/ColRoots() return the device roots.
+func (c *Context) ExtendSquare(shares [][]byte, codec rsmt2d.Codec) (*rsmt2d.ExtendedDataSquare, error) {
+	if n := len(shares); n == 0 || n&(n-1) != 0 {
+		return nil, fmt.Errorf("number of shares is not a power of 2: got %d", n)
+	}
+	flat, rr, cr, _, err := c.ExtendShares(shares)
+	if err != nil {
+		return nil, err
+	}
+	w := len(rr)
+	cells := make([][]byte, w*w)
+	for i := range cells {
+		cells[i] = flat[i*ShareSize : (i+1)*ShareSize]
+	}
+	table := &RootTable{Rows: rr, Cols: cr, Cells: cells, Width: w}
+	return rsmt2d.ImportExtendedDataSquare(cells, codec, table.NewTree)
+}
+
 // Codec implements rsmt2d.Codec (Encode/Decode/MaxChunks/Name/ValidateChunkSize) on
 // the device; rsmt2d's per-axis calls pay one launch each, so the square path above
 // is the fast path and this exists for API completeness (e.g. Repair from celestia-node).
 type Codec struct{ C *Context }
+
+var _ rsmt2d.Codec = Codec{}
 
 func (cd Codec) Name() string    { return C.GoString(C.cel_codec_name()) }
 func (cd Codec) MaxChunks() int  { return int(C.cel_codec_max_chunks()) }
@@ -129,10 +163,9 @@ func (cd Codec) Encode(data [][]byte) ([][]byte, error) {
 	for i, d := range data {
 		copy(src[i*l:], d)
 	}
-	cd.C.mu.Lock()
-	st := C.cel_codec_encode(cd.C.ctx, (*C.uint8_t)(in), C.uint32_t(n), C.uint32_t(l), (*C.uint8_t)(out))
-	cd.C.mu.Unlock()
-	if err := cd.C.err(st); err != nil {
+	if err := cd.C.call(func() C.cel_status {
+		return C.cel_codec_encode(cd.C.ctx, (*C.uint8_t)(in), C.uint32_t(n), C.uint32_t(l), (*C.uint8_t)(out))
+	}); err != nil {
 		return nil, err
 	}
 	par := unsafe.Slice((*byte)(out), n*l)
@@ -166,10 +199,9 @@ func (cd Codec) Decode(shards [][]byte) ([][]byte, error) {
 			p[i] = 0
 		}
 	}
-	cd.C.mu.Lock()
-	st := C.cel_codec_decode(cd.C.ctx, (*C.uint8_t)(buf), (*C.uint8_t)(pres), C.uint32_t(n2/2), C.uint32_t(l))
-	cd.C.mu.Unlock()
-	if err := cd.C.err(st); err != nil {
+	if err := cd.C.call(func() C.cel_status {
+		return C.cel_codec_decode(cd.C.ctx, (*C.uint8_t)(buf), (*C.uint8_t)(pres), C.uint32_t(n2/2), C.uint32_t(l))
+	}); err != nil {
 		return nil, err
 	}
 	out := make([][]byte, n2)
@@ -240,29 +272,23 @@ func (c *Context) GetCommitment(eds []byte, k, start, blobShareLen, subtreeRootT
 	buf := C.CBytes(eds)
 	defer C.free(buf)
 	out := make([]byte, 32)
-	c.mu.Lock()
-	defer c.mu.Unlock()
-	st := C.cel_get_commitment(c.ctx, (*C.uint8_t)(buf), C.uint32_t(k), C.CEL_SHARE_SIZE, C.uint32_t(start),
-		C.uint32_t(blobShareLen), C.uint32_t(subtreeRootThreshold), (*C.uint8_t)(unsafe.Pointer(&out[0])))
-	if err := c.err(st); err != nil {
+	if err := c.call(func() C.cel_status {
+		return C.cel_get_commitment(c.ctx, (*C.uint8_t)(buf), C.uint32_t(k), C.CEL_SHARE_SIZE, C.uint32_t(start),
+			C.uint32_t(blobShareLen), C.uint32_t(subtreeRootThreshold), (*C.uint8_t)(unsafe.Pointer(&out[0])))
+	}); err != nil {
 		return nil, err
 	}
 	return out, nil
 }
 
-// ByzantineError carries the axis (0 = row, 1 = column) and index rsmt2d's
-// ErrByzantineData reports; errors.Is(err, ErrByzantineData) holds.
-type ByzantineError struct {
-	Axis, Index int
-	msg         string
-}
-
-func (e *ByzantineError) Error() string { return e.msg }
-func (e *ByzantineError) Unwrap() error { return ErrByzantineData }
-
-// Repair wraps cel_repair, the device pass behind rsmt2d.ExtendedDataSquare.Repair:
-// flat is the flattened 2k x 2k square (missing cells may hold anything), present[i]
-// != 0 marks known cells. On success every cell of flat is filled in place.
+// Repair wraps cel_repair, the device pass behind rsmt2d.ExtendedDataSquare.Repair
+// (rsmt2d v0.14.0 extendeddatacrossword.go): flat is the flattened 2k x 2k square
+// (missing cells may hold anything), present[i] != 0 marks known cells. On success
+// every cell of flat is filled in place. Errors are rsmt2d's: *rsmt2d.ErrByzantineData
+// with the byzantine axis's Shares (nil where the repair did not know the cell, the
+// shares a celestia-node bad-encoding fraud proof is built from), the plain "bad root
+// input" error of preRepairSanityCheck, or rsmt2d.ErrUnrepairableDataSquare. On an
+// error present[] is left as the mask the partially repaired flat is valid under.
 func (c *Context) Repair(flat, present []byte, k int, rowRoots, colRoots [][]byte) error {
 	w := 2 * k
 	rr := make([]byte, 0, w*NmtNodeSize)
@@ -271,16 +297,26 @@ func (c *Context) Repair(flat, present []byte, k int, rowRoots, colRoots [][]byt
 		rr = append(rr, rowRoots[i]...)
 		cr = append(cr, colRoots[i]...)
 	}
+	byzShares := make([]byte, w*ShareSize)
+	byzPresent := make([]byte, w)
 	var axis, index C.int32_t
-	c.mu.Lock()
-	st := C.cel_repair(c.ctx, (*C.uint8_t)(unsafe.Pointer(&flat[0])), (*C.uint8_t)(unsafe.Pointer(&present[0])),
-		C.uint32_t(k), ShareSize, (*C.uint8_t)(unsafe.Pointer(&rr[0])), (*C.uint8_t)(unsafe.Pointer(&cr[0])),
-		&axis, &index)
-	c.mu.Unlock()
+	var st C.cel_status
+	err := c.call(func() C.cel_status {
+		st = C.cel_repair(c.ctx, (*C.uint8_t)(unsafe.Pointer(&flat[0])), (*C.uint8_t)(unsafe.Pointer(&present[0])),
+			C.uint32_t(k), ShareSize, (*C.uint8_t)(unsafe.Pointer(&rr[0])), (*C.uint8_t)(unsafe.Pointer(&cr[0])),
+			&axis, &index, (*C.uint8_t)(unsafe.Pointer(&byzShares[0])), (*C.uint8_t)(unsafe.Pointer(&byzPresent[0])))
+		return st
+	})
 	if st == C.CEL_EBYZANTINE {
-		return &ByzantineError{Axis: int(axis), Index: int(index), msg: C.GoString(C.cel_last_error(c.ctx))}
+		shares := make([][]byte, w)
+		for j := range shares {
+			if byzPresent[j] != 0 {
+				shares[j] = byzShares[j*ShareSize : (j+1)*ShareSize]
+			}
+		}
+		return &rsmt2d.ErrByzantineData{Axis: rsmt2d.Axis(axis), Index: uint(index), Shares: shares}
 	}
-	return c.err(st)
+	return err
 }
 
 // PinnedBuffer returns page-locked host memory (cel_host_alloc) for the flattened

@@ -49,6 +49,8 @@ typedef int32_t cel_status;
 #define CEL_ENOMEM 10        /* device allocation failed                                       */
 #define CEL_ESHORT 11        /* "data is too short to contain namespace ID" (nmt_wrapper.go:98) */
 #define CEL_EPUSHPAST 12     /* "pushed past predetermined square size" (nmt_wrapper.go:95)     */
+#define CEL_EBADROOT 13      /* rsmt2d preRepairSanityCheck "bad root input": a complete axis does
+                                not match its root (a plain error, not ErrByzantineData)       */
 
 /* Flags for the square entry points. */
 #define CEL_FLAG_ORDER_CHECK 0x1u   /* enforce the honest nmt push order (default in the Go path) */
@@ -183,18 +185,36 @@ cel_status cel_dah_hash(cel_ctx* ctx, const uint8_t* row_roots, const uint8_t* c
                         uint32_t w, uint8_t* out);
 
 /* ------------------------------------------------------------------ repair
- * rsmt2d ExtendedDataSquare.Repair(rowRoots, colRoots): eds is 2k*2k*share with
- * present[2k*2k] marking known cells. On CEL_OK every cell is filled. On
- * CEL_EBYZANTINE, *bad_axis (0 = row, 1 = col) and *bad_index are set. */
+ * rsmt2d ExtendedDataSquare.Repair(rowRoots, colRoots) (rsmt2d v0.14.0
+ * extendeddatacrossword.go [dep]; oracle/eds.c restates it): eds is 2k*2k*share with
+ * present[2k*2k] marking known cells.
+ *   CEL_OK            every cell filled, present[] all ones.
+ *   CEL_EBADROOT      an axis complete before the repair does not match its root
+ *                     (preRepairSanityCheck "bad root input", a plain error).
+ *   CEL_EBYZANTINE    rsmt2d *ErrByzantineData{Axis, Index, Shares}: *bad_axis (0 = row,
+ *                     1 = col), *bad_index, and (both nullable) byz_shares (2k*share) /
+ *                     byz_present (2k) = that axis's shares as rsmt2d reports them
+ *                     (absent cells zero with byz_present 0). Raised by a complete axis
+ *                     whose parity differs from Encode(data) (sanity check), a decoded axis
+ *                     failing its re-encoding or root check, or an orthogonal axis the
+ *                     decode completed failing its root or encoding.
+ *   CEL_EUNREPAIRABLE ErrUnrepairableDataSquare: no progress possible.
+ * On CEL_EBYZANTINE / CEL_EBADROOT present[] is the mask before the failing solve (the
+ * "most-repaired square prior to the byzantine axis"); on CEL_EUNREPAIRABLE the mask of
+ * the most-repaired square. Cells outside present[] are undefined. Repair checks run in
+ * rsmt2d's order (sanity: row i then column i; crossword passes over all rows, then
+ * all columns); rsmt2d runs its sanity checks in goroutines, so which failing axis it
+ * reports first is not fixed there. */
 cel_status cel_repair(cel_ctx* ctx, uint8_t* eds, uint8_t* present, uint32_t k,
                       uint32_t share_size, const uint8_t* row_roots, const uint8_t* col_roots,
-                      int32_t* bad_axis, int32_t* bad_index);
+                      int32_t* bad_axis, int32_t* bad_index, uint8_t* byz_shares,
+                      uint8_t* byz_present);
 /* Same repair over an EDS resident on ctx's device (d_eds: 2k*2k*512 bytes, filled in
- * place); present and the roots stay host memory (the crossword control loop runs on
- * the host over the presence mask). Synchronous. */
+ * place); present, the roots and the byzantine outputs stay host memory (the crossword
+ * control loop runs on the host over the presence mask). Synchronous. */
 cel_status cel_dev_repair(cel_ctx* ctx, void* d_eds, uint8_t* present, uint32_t k,
                           const uint8_t* row_roots, const uint8_t* col_roots, int32_t* bad_axis,
-                          int32_t* bad_index);
+                          int32_t* bad_index, uint8_t* byz_shares, uint8_t* byz_present);
 
 /* ------------------------------------------------------- exported trees, proofs
  * pkg/proof (proof.go:78-202, row_proof.go, share_proof.go) and the subtree-root

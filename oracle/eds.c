@@ -211,102 +211,164 @@ int orc_extend_and_commit(const uint8_t* ods, uint32_t k, size_t share, uint8_t*
 }
 
 /* -------------------------------------------------------------- repair */
+/*
+ * rsmt2d v0.14.0 ExtendedDataSquare.Repair [dep] (extendeddatacrossword.go), restated:
+ *  1. preRepairSanityCheck: every axis complete before the repair must match its root
+ *     (else ORC_EBADROOT: rsmt2d's plain "bad root input" error, not ErrByzantineData)
+ *     and its parity half must equal Encode(data half) (else ORC_EBYZANTINE, shares =
+ *     the whole axis). rsmt2d runs these checks in goroutines; this restatement fixes
+ *     the order: for i in 0..W-1: row i (root, encoding), then column i.
+ *  2. solveCrossword: passes over all rows, then all columns (each pass sees the square
+ *     as the previous pass left it), until solved or a round makes no progress
+ *     (ORC_EUNREPAIRABLE). Every incomplete axis with >= k known cells is decoded; its
+ *     parity half must equal Encode(data half) and its root must match (else
+ *     ORC_EBYZANTINE, shares = the axis before the solve, missing cells absent); then
+ *     every orthogonal axis the solve completes (in index order) must match its root
+ *     and its encoding (else ORC_EBYZANTINE, shares = that complete axis).
+ *  On ORC_EBYZANTINE / ORC_EBADROOT the presence mask is left as it was before the
+ *  failing solve ("the most-repaired square prior to the byzantine axis"); cells
+ *  outside it are undefined. byz_shares (W*share) / byz_present (W) may be NULL.
+ */
 
-/* Decode one axis (2k cells gathered from the EDS) if it is incomplete but has >= k
- * cells. Returns 1 if solved, 0 if nothing to do / not enough, <0 on byzantine. */
-static int repair_axis(uint8_t* eds, uint8_t* present, uint32_t k, size_t share, int is_col,
-                       uint32_t idx, const uint8_t* root) {
-  uint32_t w = 2 * k;
-  size_t row = (size_t)w * share;
-  size_t base = is_col ? (size_t)idx * share : (size_t)idx * row;
-  size_t stride = is_col ? row : share;
-  size_t pbase = is_col ? idx : (size_t)idx * w;
-  size_t pstride = is_col ? w : 1;
-  uint32_t have = 0;
-  for (uint32_t i = 0; i < w; i++) have += present[pbase + i * pstride] ? 1 : 0;
-  if (have == w || have < k) return 0;
-  uint8_t* cells = (uint8_t*)malloc((size_t)w * share);
-  uint8_t* pm = (uint8_t*)malloc(w);
-  for (uint32_t i = 0; i < w; i++) {
-    pm[i] = present[pbase + i * pstride];
-    if (pm[i]) memcpy(cells + (size_t)i * share, eds + base + i * stride, share);
-    else memset(cells + (size_t)i * share, 0, share);
-  }
-  int rc = orc_rs_decode(k, share, cells, pm);
-  if (rc != ORC_OK) { free(cells); free(pm); return -1; }
-  /* Re-encode check: parity recomputed from the data half must match every known cell. */
-  uint8_t* par = (uint8_t*)malloc((size_t)k * share);
-  orc_rs_encode(k, share, cells, par);
-  int bad = memcmp(par, cells + (size_t)k * share, (size_t)k * share) != 0;
+typedef struct {
+  uint8_t* eds;
+  uint8_t* present;
+  uint32_t k, w;
+  size_t share, row;
+  const uint8_t *row_roots, *col_roots;
+  int32_t *bad_axis, *bad_index;
+  uint8_t *byz_shares, *byz_present;
+} rep_t;
+
+static uint8_t* cell(const rep_t* R, int is_col, uint32_t idx, uint32_t j) {
+  return is_col ? R->eds + (size_t)j * R->row + (size_t)idx * R->share
+                : R->eds + (size_t)idx * R->row + (size_t)j * R->share;
+}
+static uint8_t* pres(const rep_t* R, int is_col, uint32_t idx, uint32_t j) {
+  return is_col ? R->present + (size_t)j * R->w + idx : R->present + (size_t)idx * R->w + j;
+}
+static uint32_t count_axis(const rep_t* R, int is_col, uint32_t idx) {
+  uint32_t c = 0;
+  for (uint32_t j = 0; j < R->w; j++) c += *pres(R, is_col, idx, j) ? 1 : 0;
+  return c;
+}
+
+/* cells: W contiguous shares of one axis. 1 = root matches. */
+static int root_ok(const rep_t* R, int is_col, uint32_t idx, const uint8_t* cells) {
+  uint8_t r[ORC_NODE];
+  orc_axis_root(cells, R->share, R->k, idx, R->share, r, 0);
+  return memcmp(r, (is_col ? R->col_roots : R->row_roots) + (size_t)idx * ORC_NODE, ORC_NODE) == 0;
+}
+/* 1 = parity half equals Encode(data half). */
+static int encoding_ok(const rep_t* R, const uint8_t* cells) {
+  size_t half = (size_t)R->k * R->share;
+  uint8_t* par = (uint8_t*)malloc(half);
+  orc_rs_encode(R->k, R->share, cells, par);
+  int ok = memcmp(par, cells + half, half) == 0;
   free(par);
-  /* Root check against the committed root. */
-  if (!bad) {
-    uint8_t r[ORC_NODE];
-    orc_axis_root(cells, share, k, idx, share, r, 0);
-    bad = memcmp(r, root, ORC_NODE) != 0;
+  return ok;
+}
+static void gather(const rep_t* R, int is_col, uint32_t idx, uint8_t* cells, uint8_t* pm) {
+  for (uint32_t j = 0; j < R->w; j++) {
+    pm[j] = *pres(R, is_col, idx, j) ? 1 : 0;
+    if (pm[j]) memcpy(cells + (size_t)j * R->share, cell(R, is_col, idx, j), R->share);
+    else memset(cells + (size_t)j * R->share, 0, R->share);
   }
-  if (bad) { free(cells); free(pm); return -1; }
-  for (uint32_t i = 0; i < w; i++)
-    if (!pm[i]) {
-      memcpy(eds + base + i * stride, cells + (size_t)i * share, share);
-      present[pbase + i * pstride] = 1;
+}
+static int byzantine(const rep_t* R, int is_col, uint32_t idx, const uint8_t* cells, const uint8_t* pm) {
+  if (R->bad_axis) *R->bad_axis = is_col;
+  if (R->bad_index) *R->bad_index = (int32_t)idx;
+  if (R->byz_shares)
+    for (uint32_t j = 0; j < R->w; j++) {
+      if (pm[j]) memcpy(R->byz_shares + (size_t)j * R->share, cells + (size_t)j * R->share, R->share);
+      else memset(R->byz_shares + (size_t)j * R->share, 0, R->share);
     }
-  free(cells);
-  free(pm);
+  if (R->byz_present) memcpy(R->byz_present, pm, R->w);
+  return ORC_EBYZANTINE;
+}
+
+static int sanity_axis(const rep_t* R, int is_col, uint32_t idx, uint8_t* cells, uint8_t* pm) {
+  if (count_axis(R, is_col, idx) != R->w) return ORC_OK;
+  gather(R, is_col, idx, cells, pm);
+  if (!root_ok(R, is_col, idx, cells)) {
+    if (R->bad_axis) *R->bad_axis = is_col;
+    if (R->bad_index) *R->bad_index = (int32_t)idx;
+    return ORC_EBADROOT;
+  }
+  if (!encoding_ok(R, cells)) return byzantine(R, is_col, idx, cells, pm);
+  return ORC_OK;
+}
+
+/* Solve one axis (>= k known, incomplete). 1 = solved, <0 = status. */
+static int solve_axis(const rep_t* R, int is_col, uint32_t idx, uint8_t* cells, uint8_t* pm, uint8_t* ocells,
+                      uint8_t* opm) {
+  gather(R, is_col, idx, cells, pm);
+  uint8_t* dec = (uint8_t*)malloc((size_t)R->w * R->share);
+  memcpy(dec, cells, (size_t)R->w * R->share);
+  int rc = orc_rs_decode(R->k, R->share, dec, pm);
+  if (rc != ORC_OK || !encoding_ok(R, dec) || !root_ok(R, is_col, idx, dec)) {
+    free(dec);
+    return -byzantine(R, is_col, idx, cells, pm);
+  }
+  /* orthogonal axes this solve completes */
+  for (uint32_t j = 0; j < R->w; j++) {
+    if (pm[j]) continue;
+    int o_col = !is_col;
+    if (count_axis(R, o_col, j) != R->w - 1) continue;
+    gather(R, o_col, j, ocells, opm);
+    memcpy(ocells + (size_t)idx * R->share, dec + (size_t)j * R->share, R->share);
+    opm[idx] = 1;
+    if (!root_ok(R, o_col, j, ocells) || !encoding_ok(R, ocells)) {
+      free(dec);
+      return -byzantine(R, o_col, j, ocells, opm);
+    }
+  }
+  for (uint32_t j = 0; j < R->w; j++)
+    if (!pm[j]) {
+      memcpy(cell(R, is_col, idx, j), dec + (size_t)j * R->share, R->share);
+      *pres(R, is_col, idx, j) = 1;
+    }
+  free(dec);
   return 1;
 }
 
 int orc_repair(uint8_t* eds, uint8_t* present, uint32_t k, size_t share, const uint8_t* row_roots,
-               const uint8_t* col_roots, int32_t* bad_axis, int32_t* bad_index) {
+               const uint8_t* col_roots, int32_t* bad_axis, int32_t* bad_index, uint8_t* byz_shares,
+               uint8_t* byz_present) {
   orc_init();
-  uint32_t w = 2 * k;
-  size_t row = (size_t)w * share;
-  /* rsmt2d prerepairSanityCheck: axes complete before the repair must match their
-   * roots (rows, then columns, in index order). */
-  for (int is_col = 0; is_col < 2; is_col++)
-    for (uint32_t i = 0; i < w; i++) {
-      uint32_t have = 0;
-      for (uint32_t j = 0; j < w; j++) have += present[is_col ? (size_t)j * w + i : (size_t)i * w + j] ? 1 : 0;
-      if (have != w) continue;
-      uint8_t r[ORC_NODE];
-      if (is_col) orc_axis_root(eds + (size_t)i * share, row, k, i, share, r, 0);
-      else orc_axis_root(eds + (size_t)i * row, share, k, i, share, r, 0);
-      if (memcmp(r, (is_col ? col_roots : row_roots) + (size_t)i * ORC_NODE, ORC_NODE) != 0) {
-        if (bad_axis) *bad_axis = is_col;
-        if (bad_index) *bad_index = (int32_t)i;
-        return ORC_EBYZANTINE;
-      }
-    }
-  /* crossword: all rows, then all columns, until solved or stuck */
-  for (;;) {
+  rep_t R = {eds, present, k, 2 * k, share, (size_t)2 * k * share, row_roots, col_roots,
+             bad_axis, bad_index, byz_shares, byz_present};
+  const uint32_t w = R.w;
+  if (bad_axis) *bad_axis = -1;
+  if (bad_index) *bad_index = -1;
+  uint8_t* cells = (uint8_t*)malloc((size_t)w * share);
+  uint8_t* ocells = (uint8_t*)malloc((size_t)w * share);
+  uint8_t* pm = (uint8_t*)malloc(w);
+  uint8_t* opm = (uint8_t*)malloc(w);
+  int rc = ORC_OK;
+  for (uint32_t i = 0; i < w && rc == ORC_OK; i++) {
+    rc = sanity_axis(&R, 0, i, cells, pm);
+    if (rc == ORC_OK) rc = sanity_axis(&R, 1, i, cells, pm);
+  }
+  while (rc == ORC_OK) {
     int progress = 0;
-    for (int is_col = 0; is_col < 2; is_col++)
+    for (int is_col = 0; is_col < 2 && rc == ORC_OK; is_col++)
       for (uint32_t i = 0; i < w; i++) {
-        int rc = repair_axis(eds, present, k, share, is_col, i,
-                             (is_col ? col_roots : row_roots) + (size_t)i * ORC_NODE);
-        if (rc < 0) {
-          if (bad_axis) *bad_axis = is_col;
-          if (bad_index) *bad_index = (int32_t)i;
-          return ORC_EBYZANTINE;
-        }
-        progress |= rc;
+        uint32_t c = count_axis(&R, is_col, i);
+        if (c == w || c < k) continue;
+        int s = solve_axis(&R, is_col, i, cells, pm, ocells, opm);
+        if (s < 0) { rc = -s; break; }
+        progress = 1;
       }
+    if (rc != ORC_OK) break;
     uint64_t have = 0;
     for (size_t i = 0; i < (size_t)w * w; i++) have += present[i] ? 1 : 0;
     if (have == (uint64_t)w * w) break;
-    if (!progress) return ORC_EUNREPAIRABLE;
+    if (!progress) rc = ORC_EUNREPAIRABLE;
   }
-  /* Final consistency: every axis root must match. */
-  for (int is_col = 0; is_col < 2; is_col++)
-    for (uint32_t i = 0; i < w; i++) {
-      uint8_t r[ORC_NODE];
-      if (is_col) orc_axis_root(eds + (size_t)i * share, row, k, i, share, r, 0);
-      else orc_axis_root(eds + (size_t)i * row, share, k, i, share, r, 0);
-      if (memcmp(r, (is_col ? col_roots : row_roots) + (size_t)i * ORC_NODE, ORC_NODE) != 0) {
-        if (bad_axis) *bad_axis = is_col;
-        if (bad_index) *bad_index = (int32_t)i;
-        return ORC_EBYZANTINE;
-      }
-    }
-  return ORC_OK;
+  free(cells);
+  free(ocells);
+  free(pm);
+  free(opm);
+  return rc;
 }

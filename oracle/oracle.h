@@ -40,6 +40,7 @@ extern "C" {
 #define ORC_ETOOFEW 6
 #define ORC_EBYZANTINE 7
 #define ORC_EUNREPAIRABLE 8
+#define ORC_EBADROOT 13 /* rsmt2d preRepairSanityCheck "bad root input" (not ErrByzantineData) */
 
 #define ORC_NS 29
 #define ORC_NODE 90
@@ -92,12 +93,15 @@ void orc_dah_hash(const uint8_t* row_roots, const uint8_t* col_roots, uint32_t w
 int orc_extend_and_commit(const uint8_t* ods, uint32_t k, size_t share, uint8_t* eds,
                           uint8_t* row_roots, uint8_t* col_roots, uint8_t dah[32]);
 
-/* rsmt2d-style Repair: eds (2k*2k*share) with present mask (2k*2k). On success every
- * cell is filled and present[] set to all ones. On EBYZANTINE, bad_axis (0 row, 1 col)
- * and bad_index are set. */
+/* rsmt2d v0.14.0 Repair (eds.c has the full restatement): eds (2k*2k*share) with present
+ * mask (2k*2k). On success every cell is filled and present[] set to all ones. On
+ * EBYZANTINE / EBADROOT, bad_axis (0 row, 1 col) and bad_index are set; on EBYZANTINE
+ * byz_shares (2k*share, nullable) / byz_present (2k, nullable) get the byzantine axis's
+ * shares (rsmt2d ErrByzantineData.Shares; absent cells zero with byz_present 0), and
+ * present[] is the mask before the failing solve. */
 int orc_repair(uint8_t* eds, uint8_t* present, uint32_t k, size_t share,
                const uint8_t* row_roots, const uint8_t* col_roots, int32_t* bad_axis,
-               int32_t* bad_index);
+               int32_t* bad_index, uint8_t* byz_shares, uint8_t* byz_present);
 
 #ifdef __cplusplus
 }

@@ -16,7 +16,7 @@ _lib = None
 
 NS = 29
 NODE = 90
-OK, EINVAL, ENOTPOW2, ECHUNK, EORDER, ETOOFEW, EBYZANTINE, EUNREPAIRABLE = 0, 1, 2, 3, 5, 6, 7, 8
+OK, EINVAL, ENOTPOW2, ECHUNK, EORDER, ETOOFEW, EBYZANTINE, EUNREPAIRABLE, EBADROOT = 0, 1, 2, 3, 5, 6, 7, 8, 13
 
 
 def build():
@@ -48,7 +48,7 @@ def lib():
         l.orc_merkle_root.argtypes = [P, u32, sz, P]
         l.orc_dah_hash.argtypes = [P, P, u32, P]
         l.orc_extend_and_commit.argtypes = [P, u32, sz, P, P, P, P]
-        l.orc_repair.argtypes = [P, P, u32, sz, P, P, P, P]
+        l.orc_repair.argtypes = [P, P, u32, sz, P, P, P, P, P, P]
         l.orc_init()
         _lib = l
     return _lib
@@ -165,13 +165,19 @@ def extend_and_commit(ods: np.ndarray, want_eds=True):
     return eds, rr, cr, dah.tobytes()
 
 
-def repair(eds: np.ndarray, present: np.ndarray, row_roots, col_roots):
+def repair(eds: np.ndarray, present: np.ndarray, row_roots, col_roots, want_shares=False):
+    """rsmt2d Repair restatement (eds.c). Returns (rc, eds, present, (axis, index)), plus
+    (byz_shares (W, share), byz_present (W,)) when want_shares."""
     eds = np.ascontiguousarray(eds, dtype=np.uint8).copy()
     present = np.ascontiguousarray(present, dtype=np.uint8).copy()
     w, _, share = eds.shape
     ba, bi = ctypes.c_int32(-1), ctypes.c_int32(-1)
+    bs = np.zeros((w, share), np.uint8)
+    bp = np.zeros(w, np.uint8)
     rc = lib().orc_repair(_p(eds), _p(present), w // 2, share, _p(np.ascontiguousarray(row_roots)),
-                          _p(np.ascontiguousarray(col_roots)), ctypes.byref(ba), ctypes.byref(bi))
+                          _p(np.ascontiguousarray(col_roots)), ctypes.byref(ba), ctypes.byref(bi), _p(bs), _p(bp))
+    if want_shares:
+        return rc, eds, present, (ba.value, bi.value), (bs, bp)
     return rc, eds, present, (ba.value, bi.value)
 
 

@@ -41,8 +41,9 @@ def test_device_independent_entry_points():
     assert lib.cel_codec_max_chunks() == 32768 * 32768
     assert lib.cel_codec_validate_chunk_size(512) == L.OK
     assert lib.cel_codec_validate_chunk_size(100) == L.ECHUNK
-    assert lib.cel_codec_validate_chunk_size(0) == L.ECHUNK
+    assert lib.cel_codec_validate_chunk_size(0) == L.OK  # rsmt2d: chunkSize % 64 != 0 only
     assert lib.cel_strerror(L.ENOTPOW2).decode().startswith("number of shares is not a power of 2")
+    assert lib.cel_strerror(L.EBADROOT).decode() == "bad root input"
     assert lib.cel_dev_workspace_size(128, 1) > 0
 
 

@@ -76,8 +76,9 @@ def test_gf16_repair_k256(ctx, oracle):
     assert np.array_equal(repair(ctx, eds, present, rr, cr), eds)
 
 
-def _dev_repair(ctx, eds, present, rr, cr):
-    """cel_dev_repair over a device-resident damaged copy; returns (status, cells, bad)."""
+def _dev_repair(ctx, eds, present, rr, cr, want_shares=False):
+    """cel_dev_repair over a device-resident damaged copy; returns (status, cells, bad)
+    (+ (byz_shares, byz_present, mask after) with want_shares)."""
     import ctypes
     from hipmem import DeviceBuffer
     w = eds.shape[0]
@@ -90,9 +91,45 @@ def _dev_repair(ctx, eds, present, rr, cr):
     rra = np.ascontiguousarray(np.frombuffer(b"".join(rr), np.uint8))
     cra = np.ascontiguousarray(np.frombuffer(b"".join(cr), np.uint8))
     ba, bi = ctypes.c_int32(-1), ctypes.c_int32(-1)
+    bs = np.zeros((w, 512), np.uint8)
+    bp = np.zeros(w, np.uint8)
     P = lambda a: a.ctypes.data_as(ctypes.c_void_p)
-    st = ctx.lib.cel_dev_repair(ctx.handle, d.ptr, P(pres), k, P(rra), P(cra), ctypes.byref(ba), ctypes.byref(bi))
-    return st, d.download(eds.shape), (ba.value, bi.value)
+    st = ctx.lib.cel_dev_repair(ctx.handle, d.ptr, P(pres), k, P(rra), P(cra), ctypes.byref(ba), ctypes.byref(bi),
+                                P(bs), P(bp))
+    cells = d.download(eds.shape)
+    if want_shares:
+        return st, cells, (ba.value, bi.value), (bs, bp, pres)
+    return st, cells, (ba.value, bi.value)
+
+
+def _stack(roots):
+    return np.stack([np.frombuffer(r, np.uint8) if isinstance(r, bytes) else r for r in roots])
+
+
+def _oracle_repair(oracle, eds, present, rr, cr):
+    damaged = eds.copy()
+    damaged[present == 0] = 0
+    return oracle.repair(damaged, present, _stack(rr), _stack(cr), want_shares=True)
+
+
+def _assert_same_outcome(ctx, oracle, eds, present, rr, cr):
+    """Device repair == oracle restatement: status, failing axis, ErrByzantineData.Shares
+    (and which of them were known), the mask left behind, and the filled square."""
+    from celestia_eds import _lib
+    st, cells, bad, (bs, bp, pres) = _dev_repair(ctx, eds, present, rr, cr, want_shares=True)
+    rc, ocells, opres, obad, (obs, obp) = _oracle_repair(oracle, eds, present, rr, cr)
+    assert st == rc, (st, rc)
+    if rc in (_lib.EBYZANTINE, _lib.EBADROOT):
+        assert bad == obad
+    if rc == _lib.EBYZANTINE:
+        assert np.array_equal(bp, obp)
+        assert np.array_equal(bs[bp == 1], obs[obp == 1])
+    assert np.array_equal(pres, opres)
+    if rc == _lib.OK:
+        assert np.array_equal(cells, eds)
+    else:  # cells the mask vouches for equal the oracle's
+        assert np.array_equal(cells[pres == 1], ocells[opres == 1])
+    return st, bad, bs, bp
 
 
 @pytest.mark.parametrize("k,p", [(64, 0.55), (128, 0.55), (32, 0.25)])
@@ -106,8 +143,7 @@ def test_dev_repair_matches_oracle(ctx, oracle, k, p):
     st, cells, _ = _dev_repair(ctx, eds, present, rr, cr)
     damaged = eds.copy()
     damaged[present == 0] = 0
-    rc, _, _, _ = oracle.repair(damaged, present, np.stack([np.frombuffer(r, np.uint8) for r in rr]),
-                                np.stack([np.frombuffer(c, np.uint8) for c in cr]))
+    rc, _, _, _ = oracle.repair(damaged, present, _stack(rr), _stack(cr))
     if rc == 0:
         assert st == _lib.OK and np.array_equal(cells, eds)
     else:
@@ -161,11 +197,101 @@ def test_byzantine_axis_matches_oracle(ctx, oracle, mask):
     r, c = 7, 11  # a present cell in every mask
     present[r, c] = 1
     bad[r, c, 300] ^= 0x21
-    st, _, dbad = _dev_repair(ctx, bad, present, rr, cr)
-    damaged = bad.copy()
-    damaged[present == 0] = 0
-    rc, _, _, obad = oracle.repair(damaged, present, np.stack([np.frombuffer(x, np.uint8) for x in rr]),
-                                   np.stack([np.frombuffer(x, np.uint8) for x in cr]))
-    assert st == rc
-    if rc == _lib.EBYZANTINE:
-        assert dbad == obad
+    st, dbad, _, _ = _assert_same_outcome(ctx, oracle, bad, present, rr, cr)
+    assert st in (_lib.EBYZANTINE, _lib.OK, _lib.EBADROOT)
+
+
+# --- config 5 at its own size (k = 128): (iv) p = 0.25 unrepairable, (v) one corrupt cell
+
+
+def test_k128_p025_unrepairable(ctx, oracle):
+    from celestia_eds import _lib
+    k = 128
+    eds, rr, cr = setup(oracle, k)
+    present = (np.random.default_rng(7).random((2 * k, 2 * k)) < 0.25).astype(np.uint8)
+    st, _, _, _ = _assert_same_outcome(ctx, oracle, eds, present, rr, cr)
+    assert st == _lib.EUNREPAIRABLE
+
+
+@pytest.mark.parametrize("p", [0.55, 1.0])
+def test_k128_one_corrupt_cell(ctx, oracle, p):
+    """One corrupted cell in the k = 128 EDS under the p = 0.55 mask (a decoded axis fails
+    its re-encoding or root) and fully present (the sanity check's encoding re-check)."""
+    from celestia_eds import _lib
+    from celestia_eds.rsmt2d import ErrByzantineData, ExtendedDataSquare
+    k = 128
+    w = 2 * k
+    eds, rr, cr = setup(oracle, k)
+    present = (np.random.default_rng(7).random((w, w)) < p).astype(np.uint8)
+    r, c = 40, 77
+    present[r, c] = 1
+    bad = eds.copy()
+    bad[r, c, 300] ^= 0x21
+    st, axis, bs, bp = _assert_same_outcome(ctx, oracle, bad, present, rr, cr)
+    assert st == _lib.EBYZANTINE
+    # the host entry point raises rsmt2d's error with the same Shares
+    sq = ExtendedDataSquare(np.where(present[..., None] == 1, bad, 0).astype(np.uint8), ctx=ctx)
+    mask_in = present.copy()
+    with pytest.raises(ErrByzantineData) as ei:
+        sq.Repair(rr, cr, present=present)
+    assert np.array_equal(present, mask_in)  # the caller's mask is not written through
+    e = ei.value
+    assert (e.Axis, e.Index) == axis
+    assert [s is not None for s in e.Shares] == [bool(x) for x in bp]
+    assert all(s == bs[j].tobytes() for j, s in enumerate(e.Shares) if s is not None)
+
+
+def test_sanity_check_bad_encoding(ctx, oracle):
+    """Every cell present, row 3's parity half changed, and roots computed over that
+    square: every root matches, so only rsmt2d's re-encoding of complete axes in
+    preRepairSanityCheck catches it (ErrByzantineData, row 3, all its shares)."""
+    from celestia_eds import _lib
+    k = 16
+    w = 2 * k
+    eds, _, _ = setup(oracle, k, seed=3)
+    eds[3, k + 1, 100] ^= 0x77  # Q1 cell: row 3 and column k + 1 are no longer codewords
+    _, rr, cr = oracle.roots(eds, check_order=False)
+    present = np.ones((w, w), np.uint8)
+    st, bad, bs, bp = _assert_same_outcome(ctx, oracle, eds, present, [x.tobytes() for x in rr],
+                                           [x.tobytes() for x in cr])
+    assert st == _lib.EBYZANTINE and bad == (0, 3)
+    assert bp.all() and np.array_equal(bs, eds[3])
+
+
+def test_sanity_check_bad_root(ctx, oracle):
+    """A complete row whose root differs: rsmt2d's "bad root input", not ErrByzantineData."""
+    from celestia_eds import CelError, _lib
+    from celestia_eds.rsmt2d import ExtendedDataSquare
+    k = 8
+    eds, rr, cr = setup(oracle, k)
+    rr = list(rr)
+    rr[5] = bytes(90)
+    present = np.ones((2 * k, 2 * k), np.uint8)
+    present[0, 0] = 0
+    st, bad, _, _ = _assert_same_outcome(ctx, oracle, eds, present, rr, cr)
+    assert st == _lib.EBADROOT and bad == (0, 5)
+    with pytest.raises(CelError) as ei:
+        ExtendedDataSquare(eds.copy(), ctx=ctx).Repair(rr, cr, present=present)
+    assert ei.value.status == _lib.EBADROOT and "bad root input" in str(ei.value)
+
+
+def test_orthogonal_completion_then_stuck(ctx, oracle):
+    """Row r0 decodes and completes column c, whose known cell (r1, c) is corrupted (the
+    roots were computed over the corrupted square, so every root matches); nothing else is
+    solvable. rsmt2d's check of the newly completed column reports ErrByzantineData(Col, c)
+    although the repair is stuck afterwards."""
+    from celestia_eds import _lib
+    k = 16
+    w = 2 * k
+    r0, r1, c = 2, 9, 5
+    eds, _, _ = setup(oracle, k, seed=4)
+    eds[r1, c, 200] ^= 0x10
+    _, rr, cr = oracle.roots(eds, check_order=False)
+    present = np.zeros((w, w), np.uint8)
+    present[:, c] = 1
+    present[r0, :] = 0
+    present[r0, k:] = 1  # k cells of row r0, not column c
+    st, bad, bs, bp = _assert_same_outcome(ctx, oracle, eds, present, [x.tobytes() for x in rr],
+                                           [x.tobytes() for x in cr])
+    assert st == _lib.EBYZANTINE and bad == (1, c)
+    assert bp.all() and np.array_equal(bs, eds[:, c])

@@ -125,13 +125,55 @@ def test_repair_semantics(oracle):
     present[0, :k - 1] = 1
     rc, _, _, _ = oracle.repair(damaged, present, rr, cr)
     assert rc == oracle.EUNREPAIRABLE
-    # one corrupted cell: byzantine
+    # one corrupted cell of a complete row: rsmt2d's "bad root input" (a plain error)
     present = np.ones((w, w), np.uint8)
     present[1, 1] = 0
     bad = eds.copy()
     bad[0, 0, 100] ^= 1
     rc, _, _, (ba, bi) = oracle.repair(bad, present, rr, cr)
-    assert rc == oracle.EBYZANTINE and ba in (0, 1) and bi >= 0
+    assert rc == oracle.EBADROOT and (ba, bi) == (0, 0)
+    # the corrupted cell inside an incomplete row: the decoded row fails -> byzantine,
+    # Shares = that row before the solve
+    present[0, 3] = 0
+    present[5, 0] = 0  # column 0 incomplete as well
+    rc, _, pres, (ba, bi), (bs, bp) = oracle.repair(bad, present, rr, cr, want_shares=True)
+    assert rc == oracle.EBYZANTINE and (ba, bi) == (0, 0)
+    assert np.array_equal(bp, present[0]) and np.array_equal(bs[0], bad[0, 0])
+    assert np.array_equal(pres, present)  # nothing solved before row 0
+
+
+def test_repair_sanity_encoding_check(oracle):
+    """rsmt2d preRepairSanityCheck re-encodes complete axes: a square whose row 3 is not a
+    codeword, with roots computed over it, is ErrByzantineData(Row, 3)."""
+    k = 8
+    w = 2 * k
+    eds, _, _, _ = oracle.extend_and_commit(random_ods(k, 12))
+    eds[3, k + 2, 50] ^= 0x80
+    _, rr, cr = oracle.roots(eds, check_order=False)
+    rc, _, _, bad, (bs, bp) = oracle.repair(eds, np.ones((w, w), np.uint8), rr, cr, want_shares=True)
+    assert rc == oracle.EBYZANTINE and bad == (0, 3) and bp.all() and np.array_equal(bs, eds[3])
+
+
+def test_repair_orthogonal_completion(oracle):
+    """The orthogonal axis a solve completes is checked at once (root and encoding), so a
+    square that is stuck afterwards still reports ErrByzantineData for that column."""
+    k = 8
+    w = 2 * k
+    r0, r1, c = 1, 6, 4
+    eds, _, _, _ = oracle.extend_and_commit(random_ods(k, 13))
+    eds[r1, c, 100] ^= 0x04
+    _, rr, cr = oracle.roots(eds, check_order=False)
+    present = np.zeros((w, w), np.uint8)
+    present[:, c] = 1
+    present[r0, :] = 0
+    present[r0, k:] = 1
+    rc, _, pres, bad, (bs, bp) = oracle.repair(eds, present, rr, cr, want_shares=True)
+    assert rc == oracle.EBYZANTINE and bad == (1, c) and bp.all() and np.array_equal(bs, eds[:, c])
+    assert np.array_equal(pres, present)  # the mask before row r0's solve
+    # without the corruption the same mask is simply unrepairable
+    eds2, rr2, cr2, _ = oracle.extend_and_commit(random_ods(k, 13))
+    rc, _, _, _ = oracle.repair(eds2, present, rr2, cr2)
+    assert rc == oracle.EUNREPAIRABLE
 
 
 def test_nmt_empty_root(oracle):

@@ -1,0 +1,60 @@
+"""Host logic of the Python rsmt2d mirror (no device): custom tree constructors are
+honoured the way rsmt2d honours them (pkg/inclusion/nmt_caching.go:96-104,
+test/util/malicious/tree.go:36-71 pass their own TreeConstructorFn), and a codec other
+than Leopard is refused instead of being silently replaced by the device codec."""
+import hashlib
+
+import numpy as np
+import pytest
+
+
+class CountingTree:
+    """A stand-in TreeConstructorFn tree: its root is sha256 over what was pushed."""
+
+    calls = []
+
+    def __init__(self, axis, index):
+        self.axis, self.index, self.h = axis, index, hashlib.sha256()
+        CountingTree.calls.append((axis, index))
+
+    def Push(self, data):
+        self.h.update(bytes(data))
+
+    def Root(self):
+        return self.h.digest()
+
+
+def test_custom_tree_constructor_is_honoured():
+    from celestia_eds.rsmt2d import Col, ImportExtendedDataSquare, Row
+    w = 4
+    rng = np.random.default_rng(1)
+    cells = rng.integers(0, 256, (w, w, 512), dtype=np.uint8)
+    CountingTree.calls = []
+    eds = ImportExtendedDataSquare([cells[r, c].tobytes() for r in range(w) for c in range(w)],
+                                   tree_constructor=CountingTree)
+    rows, cols = eds.RowRoots(), eds.ColRoots()
+    assert rows[1] == hashlib.sha256(cells[1].tobytes()).digest()
+    assert cols[2] == hashlib.sha256(cells[:, 2].tobytes()).digest()
+    assert sorted(CountingTree.calls) == sorted([(Row, i) for i in range(w)] + [(Col, i) for i in range(w)])
+
+
+def test_default_wrapper_constructor_is_recognised():
+    from celestia_eds import wrapper
+    from celestia_eds.rsmt2d import _default_constructor
+    assert _default_constructor(None)
+    assert _default_constructor(wrapper.NewConstructor(4))
+    assert not _default_constructor(CountingTree)
+
+
+def test_foreign_codec_is_refused():
+    from celestia_eds import CelError, _lib
+    from celestia_eds.rsmt2d import ComputeExtendedDataSquare, ImportExtendedDataSquare
+
+    class RSGF8Codec:  # e.g. rsmt2d.NewRSGF8Codec()
+        pass
+
+    with pytest.raises(CelError) as ei:
+        ImportExtendedDataSquare([bytes(512)] * 4, codec=RSGF8Codec())
+    assert ei.value.status == _lib.EINVAL
+    with pytest.raises(CelError):
+        ComputeExtendedDataSquare([bytes(512)], codec=RSGF8Codec())
