@@ -5,7 +5,9 @@ k x k squares already resident in HBM (RS extension to the 2k x 2k EDS, 4k NMT
 roots, DAH hash), through the C ABI's device-resident entry point. Multi-GPU runs
 are batch/replay mode: every rank extends its own squares, no data-path
 collective (weak scaling); the barrier and max-over-ranks timing follow the driver
-contract.
+contract. `--gpus N` without torchrun's environment relaunches this script under
+`torch.distributed.run` with N ranks (before anything touches a GPU), so
+`python bench.py --gpus 8` and the driver's torchrun line run the same code.
 
 Besides the headline number the JSON line carries:
   roofline      RS extension (both passes) vs HBM: algorithmic 2048 k^2 bytes per
@@ -16,10 +18,15 @@ Besides the headline number the JSON line carries:
                 squares (GF(2^16)), since the metric names k=128 and k=512
   cpu_baseline  the C restatement (oracle/, SIMD + OpenMP) on a bounded sample of the
                 same squares, rank 0 at N = 1 only; its DAHs also cross-check the GPU
+  host_io       the PCIe-inclusive rate of the host-buffer entry point (cel_extend_batch)
+                that the Go shim behind da.ExtendShares calls: EDS copied back, and
+                roots + DAH only (rank 0 at N = 1; never the headline value)
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -74,13 +81,80 @@ def parse():
     ap.add_argument("--k512-batch", type=int, default=32,
                     help="with --k 128: k=512 squares per step per GPU of the companion line (0 = off)")
     ap.add_argument("--k512-steps", type=int, default=5)
-    ap.add_argument("--mode", default="batch", choices=["batch", "sharded", "repair"],
+    ap.add_argument("--mode", default="batch", choices=["batch", "sharded", "repair", "distcheck"],
                     help="batch: independent squares per GPU (configs 2, 4); sharded: one square "
-                         "row-sharded over the ranks (config 3); repair: rsmt2d Repair (config 5)")
+                         "row-sharded over the ranks (config 3); repair: rsmt2d Repair (config 5); "
+                         "distcheck: the launcher / rendezvous / timing contract on CPU ranks over gloo "
+                         "(no GPU work; used by the CPU tests)")
+    ap.add_argument("--no-host-io", action="store_true", help="skip the host_io (PCIe-inclusive) measurement")
     ap.add_argument("--repair-p", type=float, default=0.55, help="repair mode: cell survival probability")
     ap.add_argument("--repair-input", default="device", choices=["device", "host"],
                     help="repair mode: EDS resident in HBM (cel_dev_repair) or host buffers (cel_repair, PCIe)")
     return ap.parse_args()
+
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch(a):
+    """--gpus N > 1 without torchrun's environment: run this script under
+    torch.distributed.run with N ranks (one per GPU, rendezvous on 127.0.0.1) as a child
+    process and return its exit code. Nothing has touched a GPU in this process."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // a.gpus)))
+    return subprocess.call(cmd, env=env)
+
+
+def _dist_env():
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def run_distcheck(a):
+    """The multi-rank contract without a GPU: gloo rendezvous, W untimed + K timed steps
+    bracketed by barriers, MAX over ranks, one JSON line from rank 0 with n_gpus = world.
+    A step is a fixed CPU hash of a rank-local buffer (a stand-in for the batch step)."""
+    import hashlib
+    import torch.distributed as dist
+    world, rank, _ = _dist_env()
+    if world > 1:
+        dist.init_process_group("gloo")
+    buf = np.random.default_rng(rank).integers(0, 256, 1 << 20, dtype=np.uint8).tobytes()
+
+    def step():
+        hashlib.sha256(buf).digest()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(a.warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank == 0:
+        print(json.dumps({"metric": "distcheck steps/sec", "value": world * a.steps / elapsed, "unit": "steps/s",
+                          "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+                          "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+                          "vs_baseline": None, "dtype": "u8", "data": "synthetic (CPU stand-in step, gloo)",
+                          "config": {"workload": "launcher / rendezvous / timing contract check",
+                                     "parallelism": f"batch{world}"}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def _cpu_cores():
@@ -99,9 +173,7 @@ def run_sharded(a):
     all_to_all_single transposes them into column slabs, each rank column-encodes and
     hashes its slab, two all-gathers of 96-byte records and a combine give the roots
     and the DAH on every rank. At N = 1 the same schedule runs without collectives."""
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = _dist_env()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     from celestia_eds import default_context
@@ -210,9 +282,14 @@ def run_sharded(a):
 def run_repair(a):
     """Config 5: rsmt2d Repair of a k x k EDS from a random sample (cells kept with
     probability --repair-p, seed 7): crossword erasure decode on the device, re-encode
-    check and root re-verification. --repair-input device (default): the damaged EDS
-    resident in HBM (cel_dev_repair), a fresh damaged copy made inside every step;
-    host: host buffers in and out (cel_repair), PCIe copies included. Single rank."""
+    checks and root re-verification. --repair-input device (default): the damaged EDS
+    resident in HBM (cel_dev_repair); the fresh damaged copy each step needs is made
+    before the step's clock starts. host: host buffers in and out (cel_repair), PCIe
+    copies included. Single rank.
+    roofline: k_rs_decode alone (cel_dev_decode over the row pass's axes of the same
+    mask), algorithmic bytes = every shard of every decoded axis read once + every
+    missing shard written once, against HBM; the decoder is VALU/LDS-bound (its twiddle
+    tables come from LDS per butterfly), so the fraction says how far from streaming."""
     torch.cuda.set_device(0)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
@@ -228,38 +305,68 @@ def run_repair(a):
     damaged[present == 0] = 0
     ctx = default_context(0)
     rrl, crl = [r.tobytes() for r in rr], [c.tobytes() for c in cr]
+    import ctypes
+    P = lambda x: x.ctypes.data_as(ctypes.c_void_p)
 
     if a.repair_input == "host":
-        def once():
-            sq = ExtendedDataSquare(damaged.copy(), ctx=ctx)
-            sq.Repair(rrl, crl, present=present.copy())
+        def prepare():
+            return ExtendedDataSquare(damaged.copy(), ctx=ctx)
+
+        def once(sq):
+            sq.Repair(rrl, crl, present=present)
             return sq.cells
     else:
-        import ctypes
         d_damaged = torch.from_numpy(damaged).cuda()
         d_work = torch.empty_like(d_damaged)
         rra, cra = np.ascontiguousarray(rr), np.ascontiguousarray(cr)
-        P = lambda x: x.ctypes.data_as(ctypes.c_void_p)
 
-        def once():
-            # fresh damaged copy (32 MiB D2D at k=128, inside the timed step), then the repair
-            d_work.copy_(d_damaged)
-            torch.cuda.current_stream().synchronize()
-            pres = present.copy()
+        def prepare():
+            d_work.copy_(d_damaged)  # 32 MiB D2D at k = 128, outside the step's clock
+            torch.cuda.synchronize()
+            return present.copy()
+
+        def once(pres):
             ctx.check(ctx.lib.cel_dev_repair(ctx.handle, ctypes.c_void_p(d_work.data_ptr()), P(pres), k, P(rra),
                                              P(cra), None, None, None, None))
             return d_work
 
     for _ in range(a.warmup):
-        once()
+        once(prepare())
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
+    elapsed = 0.0
     for _ in range(a.steps):
-        out = once()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+        arg = prepare()
+        t0 = time.perf_counter()
+        out = once(arg)  # cel_dev_repair / cel_repair are synchronous
+        torch.cuda.synchronize()
+        elapsed += time.perf_counter() - t0
     cells = out if isinstance(out, np.ndarray) else out.cpu().numpy()
     assert np.array_equal(cells, eds), "repaired EDS differs"
+    # decode roofline: the row pass's decode (every row with >= k and < 2k known cells)
+    rows = [i for i in range(w) if k <= int(present[i].sum()) < w]
+    dense = torch.from_numpy(np.ascontiguousarray(damaged[rows])).cuda()
+    dmask = torch.from_numpy(np.ascontiguousarray(present[rows])).cuda()
+    scratch = torch.empty_like(dense)
+    stream = torch.cuda.Stream()
+    sp = ctypes.c_void_p(stream.cuda_stream)
+
+    def decode():
+        ctx.check(ctx.lib.cel_dev_decode(ctx.handle, ctypes.c_void_p(scratch.data_ptr()),
+                                         ctypes.c_void_p(dmask.data_ptr()), len(rows), k, 512, sp))
+
+    reps = max(3, a.phase_reps)
+    scratch.copy_(dense)
+    torch.cuda.synchronize()
+    decode()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        decode()  # re-decoding a decoded axis repeats the same work
+    e1.record(stream)
+    e1.synchronize()
+    t_dec = e0.elapsed_time(e1) / reps / 1e3
+    missing = int((present[rows] == 0).sum())
+    dec_bytes = len(rows) * w * 512 + missing * 512
     n_cpu, t_cpu = 0, 0.0
     while t_cpu < min(a.cpu_seconds, 10.0) and n_cpu < 20:
         t1 = time.perf_counter()
@@ -275,8 +382,15 @@ def run_repair(a):
         "vs_baseline": None, "dtype": "u8", "data": "synthetic (testfactory-style ODS, random survival mask)",
         "config": {"workload": f"Repair k={k} EDS from {present.mean():.3f} of its cells "
                                + ("(host buffers, PCIe included)" if a.repair_input == "host"
-                                  else "(EDS resident in HBM, fresh damaged copy per step)"),
+                                  else "(EDS resident in HBM; the damaged-copy restore runs before each step's "
+                                       "clock)"),
                    "k": k, "parallelism": "single"},
+        "roofline": {"bound": "hbm", "kernel": "k_rs_decode (cel_dev_decode, the row pass's axes)",
+                     "achieved": dec_bytes / t_dec / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": dec_bytes / t_dec / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                     "avg_launch_us": t_dec * 1e6, "axes": len(rows),
+                     "bytes_per_launch": dec_bytes,
+                     "bytes_basis": "every shard of each decoded axis read once + each missing shard written once"},
         "cpu_baseline": {"value": n_cpu / t_cpu, "unit": "squares/s", "cores": oracle.lib().orc_get_threads(),
                          "kind": "port", "sample": f"{n_cpu} repairs of the same damaged square (C restatement)"},
     }), flush=True)
@@ -332,15 +446,62 @@ def _measure_batch(ctx, local, rank, k, B, steps, warmup, n_distinct, layout, ph
     return {"sb": sb, "distinct": distinct, "elapsed": elapsed, "t_ext": t_ext, "t_com": t_com}
 
 
+def measure_host_io(ctx, k, n=16, reps=3):
+    """cel_extend_batch over page-locked host buffers (cel_host_alloc): n ODSs in, then
+    (a) the EDS + roots + DAH out (what rsmt2d.ImportExtendedDataSquare needs) and
+    (b) roots + DAH only (PrepareProposal/ProcessProposal keep only the DAH,
+    app/prepare_proposal.go:81-83). PCIe copies included; never the headline value."""
+    import ctypes
+    from celestia_eds import _lib
+    from celestia_eds.testfactory import random_ods
+    w = 2 * k
+
+    def pinned(shape):
+        nbytes = int(np.prod(shape))
+        p = ctx.lib.cel_host_alloc(nbytes)
+        assert p, "cel_host_alloc failed"
+        return p, np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p)).reshape(shape)
+
+    p_ods, ods = pinned((n, k, k, 512))
+    ods[...] = np.stack([random_ods(k, 500 + i) for i in range(n)])
+    p_eds, eds = pinned((n, w, w, 512))
+    rr = np.zeros((n, w, 90), np.uint8)
+    cr = np.zeros_like(rr)
+    dah = np.zeros((n, 32), np.uint8)
+    st = np.zeros(n, np.int32)
+    P = lambda x: x.ctypes.data_as(ctypes.c_void_p)
+    out = {}
+    try:
+        for name, e in (("with_eds", eds), ("roots_only", None)):
+            def once():
+                ctx.check(ctx.lib.cel_extend_batch(ctx.handle, P(ods), n, k, 512, P(e) if e is not None else None,
+                                                   P(rr), P(cr), P(dah), P(st), _lib.FLAG_ORDER_CHECK))
+            once()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                once()
+            dt = (time.perf_counter() - t0) / reps
+            pcie = ods.nbytes + (eds.nbytes if e is not None else 0) + rr.nbytes + cr.nbytes
+            out[name] = {"squares_per_s": n / dt, "pcie_gbps": pcie / dt / 1e9, "ms_per_call": dt * 1e3}
+    finally:
+        ctx.lib.cel_host_free(p_ods)
+        ctx.lib.cel_host_free(p_eds)
+    out["squares_per_call"] = n
+    out["entry_point"] = "cel_extend_batch (host buffers, page-locked, 4 chunks over the ctx streams)"
+    return out
+
+
 def main():
     a = parse()
+    world, rank, local = _dist_env()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(a))
+    if a.mode == "distcheck":
+        return run_distcheck(a)
     if a.mode == "sharded":
         return run_sharded(a)
     if a.mode == "repair":
         return run_repair(a)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
@@ -441,6 +602,8 @@ def main():
         sb = None
     else:
         dah128 = None
+    if rank == 0 and world == 1 and a.k == 128 and not a.no_host_io:
+        result["host_io"] = measure_host_io(ctx, a.k)
     if rank == 0 and world == 1 and not a.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle

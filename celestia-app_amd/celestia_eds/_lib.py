@@ -24,7 +24,7 @@ NMT_NODE_SIZE = 90
 EXPORTS = [
     "cel_ctx_create", "cel_ctx_destroy", "cel_strerror", "cel_last_error", "cel_device_name",
     "cel_extend_shares", "cel_extend_batch", "cel_dev_workspace_size", "cel_dev_extend_batch",
-    "cel_dev_extend_only", "cel_dev_commit_only", "cel_dev_place_ods", "cel_host_alloc", "cel_host_free", "cel_codec_encode", "cel_codec_decode",
+    "cel_dev_extend_only", "cel_dev_commit_only", "cel_dev_place_ods", "cel_dev_decode", "cel_host_alloc", "cel_host_free", "cel_codec_encode", "cel_codec_decode",
     "cel_codec_max_chunks", "cel_codec_name", "cel_codec_validate_chunk_size", "cel_axis_root",
     "cel_nmt_root", "cel_dah_hash", "cel_repair", "cel_dev_repair", "cel_dev_shard_workspace_size", "cel_dev_shard_rows",
     "cel_dev_shard_cols", "cel_dev_shard_finish", "cel_square_construct", "cel_square_last_error", "cel_square_tx_range",
@@ -70,6 +70,7 @@ def load():
             "cel_dev_commit_only": (i32, [P, P, u32, u32, P, P, P, P, P, P, u32]),
             "cel_codec_encode": (i32, [P, P, u32, u32, P]),
             "cel_codec_decode": (i32, [P, P, P, u32, u32]),
+            "cel_dev_decode": (i32, [P, P, P, u32, u32, u32, P]),
             "cel_codec_max_chunks": (u64, []),
             "cel_codec_name": (ctypes.c_char_p, []),
             "cel_codec_validate_chunk_size": (i32, [u32]),

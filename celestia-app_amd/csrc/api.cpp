@@ -576,6 +576,20 @@ cel_status cel_codec_decode(cel_ctx* ctx, uint8_t* shards, const uint8_t* presen
   return CEL_OK;
 }
 
+cel_status cel_dev_decode(cel_ctx* ctx, void* d_shards, const void* d_present, uint32_t naxes, uint32_t n,
+                          uint32_t len, void* stream) {
+  if (!ctx) return CEL_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (!d_shards || !d_present || !naxes || !n) return fail(ctx, CEL_EINVAL, "nil argument");
+  if (len == 0 || cel_codec_validate_chunk_size(len)) return fail(ctx, CEL_ECHUNK, "shard size must be a multiple of 64");
+  if (!is_pow2(n)) return fail(ctx, CEL_ENOTPOW2, "number of data shards is not a power of 2");
+  if (n > 1024) return fail(ctx, CEL_ETOOBIG, "too many shards for the device decoder");
+  DeviceGuard g(ctx->device);
+  const hipError_t e = launch_rs_decode(static_cast<uint8_t*>(d_shards), static_cast<const uint8_t*>(d_present), naxes,
+                                        n, len, ctx->tables, nullptr, pick_stream(ctx, stream));
+  return e == hipSuccess ? CEL_OK : hip_fail(ctx, e, "decode");
+}
+
 // -------------------------------------------------------------------- trees
 
 cel_status cel_axis_root(cel_ctx* ctx, const uint8_t* cells, uint32_t k, uint32_t axis_index, uint32_t share_size,
@@ -890,11 +904,14 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
   auto at = [&](int is_col, uint32_t i, uint32_t j) -> uint8_t& {
     return is_col ? hm[(size_t)j * W + i] : hm[(size_t)i * W + j];
   };
-  auto count = [&](int is_col, uint32_t i) {
-    uint32_t c = 0;
-    for (uint32_t j = 0; j < W; j++) c += at(is_col, i, j);
-    return c;
-  };
+  std::vector<uint32_t> cnt[2] = {std::vector<uint32_t>(W, 0), std::vector<uint32_t>(W, 0)};  // known cells per axis
+  for (uint32_t i = 0; i < W; i++)
+    for (uint32_t j = 0; j < W; j++)
+      if (hm[(size_t)i * W + j]) {
+        cnt[0][i]++;
+        cnt[1][j]++;
+      }
+  auto count = [&](int is_col, uint32_t i) { return cnt[is_col][i]; };
   std::vector<Check> order;
   std::vector<Solve> solves;
   std::vector<std::vector<int32_t>> lists;  // kept alive until the final sync
@@ -934,7 +951,8 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
         for (uint32_t j = 0; j < W; j++) {
           if (sv.before[j]) continue;
           at(is_col, (uint32_t)i, j) = 1;
-          if (count(!is_col, j) == W) {
+          cnt[is_col][i]++;
+          if (++cnt[!is_col][j] == W) {
             order.push_back({Check::ORTH, !is_col, (int32_t)j, si});
             orth.push_back((int32_t)j);
           }
@@ -948,7 +966,7 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
       progress = true;
     }
     size_t have = 0;
-    for (size_t i = 0; i < cells; i++) have += hm[i];
+    for (uint32_t i = 0; i < W; i++) have += cnt[0][i];
     if (have == cells) {
       solved = true;
       break;

@@ -167,6 +167,12 @@ cel_status cel_codec_encode(cel_ctx* ctx, const uint8_t* data, uint32_t n, uint3
  * Fills every missing shard in place (rsmt2d Codec.Decode). */
 cel_status cel_codec_decode(cel_ctx* ctx, uint8_t* shards, const uint8_t* present, uint32_t n,
                             uint32_t len);
+/* Device-resident batch of rsmt2d Codec.Decode calls (one per axis), as the repair's
+ * crossword passes issue them: d_shards [naxes][2n][len] (data then parity, filled in
+ * place), d_present [naxes][2n] (0 = missing; every axis needs >= n present). n <= 1024,
+ * len a positive multiple of 64. Asynchronous on stream (NULL = ctx's stream). */
+cel_status cel_dev_decode(cel_ctx* ctx, void* d_shards, const void* d_present, uint32_t naxes, uint32_t n,
+                          uint32_t len, void* stream);
 uint64_t cel_codec_max_chunks(void);             /* 32768 * 32768 */
 const char* cel_codec_name(void);                /* "Leopard" */
 cel_status cel_codec_validate_chunk_size(uint32_t len);

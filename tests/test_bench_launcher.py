@@ -1,0 +1,36 @@
+"""bench.py --gpus N relaunches itself under torch.distributed.run with N ranks (the
+driver's N-GPU line); the distcheck mode runs that same launcher,
+rendezvous (gloo, 127.0.0.1), barrier + MAX-over-ranks timing and rank-0 JSON path on
+CPU ranks."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, timeout=240):
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    env.pop("LOCAL_RANK", None)
+    env["OMP_NUM_THREADS"] = "1"
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=timeout, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    return [json.loads(l) for l in lines]
+
+
+def test_launcher_two_ranks():
+    out = _run(["--gpus", "2", "--mode", "distcheck", "--steps", "3", "--warmup", "1"])
+    assert len(out) == 1, out
+    r = out[0]
+    assert r["n_gpus"] == 2 and r["steps"] == 3 and r["warmup"] == 1
+    assert r["value"] > 0 and r["scaling"] == "weak" and r["config"]["parallelism"] == "batch2"
+
+
+def test_single_rank_no_relaunch():
+    out = _run(["--mode", "distcheck", "--steps", "2", "--warmup", "0"])
+    assert len(out) == 1 and out[0]["n_gpus"] == 1

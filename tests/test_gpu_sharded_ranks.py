@@ -1,0 +1,73 @@
+"""The row-sharded square (config 3) with real processes and a real collective: two
+ranks, each driving the HIP device steps (cel_dev_shard_*) on the box's GPU, exchanging
+the all-to-all blocks and the record all-gathers through torch.distributed (gloo over
+TCP, the device tensors staged through host memory because gloo has no all_to_all for
+device tensors). The result must equal the oracle's whole-square roots and DAH. On the
+8-GPU node the same ShardedSquare.run drives RCCL (bench.py --mode sharded)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+class StagedComm:
+    """torch.distributed gloo collectives on host copies of device tensors."""
+
+    def __init__(self):
+        import torch.distributed as dist
+        self.dist = dist
+
+    def all_to_all(self, out, inp):
+        h_out = out.cpu()
+        self.dist.all_to_all_single(h_out, inp.cpu())
+        out.copy_(h_out)
+
+    def all_gather(self, out, inp):
+        h_out = out.cpu()
+        self.dist.all_gather_into_tensor(h_out, inp.cpu())
+        out.copy_(h_out)
+
+    def all_reduce_max(self, t):
+        h = t.cpu()
+        self.dist.all_reduce(h, op=self.dist.ReduceOp.MAX)
+        t.copy_(h)
+
+
+def _worker(rank, world, port, k, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch
+    import torch.distributed as dist
+    from celestia_eds import default_context
+    from celestia_eds.sharded import DeviceSteps, ShardedSquare
+    from celestia_eds.testfactory import random_ods
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    steps = DeviceSteps(default_context(0), 0)
+    sq = ShardedSquare(k, rank, world, steps)
+    lo, hi = sq.row_range()
+    sq.ods_rows.copy_(torch.from_numpy(np.ascontiguousarray(random_ods(k, 77)[lo:hi])))
+    sq.run(StagedComm())
+    torch.cuda.synchronize()
+    sq.check_status()
+    np.savez(os.path.join(outdir, f"r{rank}.npz"), rr=sq.row_roots.cpu().numpy(), cr=sq.col_roots.cpu().numpy(),
+             dah=sq.dah.cpu().numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_processes_gloo(oracle, tmp_path):
+    import torch.multiprocessing as mp
+    from celestia_eds.testfactory import random_ods
+    k, world = 256, 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_worker, args=(world, port, k, str(tmp_path)), nprocs=world, join=True)
+    _, rr, cr, dah = oracle.extend_and_commit(random_ods(k, 77), want_eds=False)
+    for r in range(world):
+        got = np.load(tmp_path / f"r{r}.npz")
+        assert np.array_equal(got["rr"], rr) and np.array_equal(got["cr"], cr)
+        assert got["dah"].tobytes() == dah

@@ -1,21 +1,17 @@
 #!/bin/bash
-# Full round check: GPU parity tests -> smoke -> default bench (with CPU baseline)
-# -> rocprofv3 kernel-trace stats of the same bench. Each GPU step has its own limit;
-# any crash/abort/timeout stops the script.
-set -u
-cd "$(dirname "$0")/.."
+# One GPU-box pass: the -m gpu parity suite, then the default bench line and the repair
+# line. Every step has its own time limit; the chain stops at the first failure.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
-export TMPDIR=/tmp
-TAG=${TAG:-run}
-timeout -k 10 ${PYTEST_TIMEOUT:-420} python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread \
-  ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu_$TAG.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/pytest_gpu_$TAG.log; case $rc in 0|1) ;; *) exit $rc ;; esac
-timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1
-rc=$?; echo "smoke rc=$rc"; tail -2 gpurun_out/smoke_$TAG.log; [ $rc -le 1 ] || exit $rc
-timeout -k 10 240 python -u bench.py ${BENCH_ARGS:-} > gpurun_out/bench_$TAG.log 2>&1
-rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench_$TAG.log | cut -c1-1500; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- \
-  python3 bench.py --no-cpu ${BENCH_ARGS:-} > gpurun_out/bench_prof_$TAG.log 2>&1
-rc=$?; echo "prof rc=$rc"
-python3 tools/kstats.py gpurun_out/prof_$TAG
-exit $rc
+tag=${1:-r2}
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+  > gpurun_out/${tag}_pytest_gpu.log 2>&1
+rc=$?
+tail -5 gpurun_out/${tag}_pytest_gpu.log
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+timeout -k 10 300 python -u bench.py > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err || exit $?
+cat gpurun_out/${tag}_bench.json
+timeout -k 10 300 python -u bench.py --mode repair --steps 20 --warmup 3 \
+  > gpurun_out/${tag}_bench_repair.json 2> gpurun_out/${tag}_bench_repair.err || exit $?
+cat gpurun_out/${tag}_bench_repair.json
