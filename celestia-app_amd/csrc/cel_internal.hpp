@@ -73,6 +73,7 @@ hipError_t launch_rs_encode(const RsGeom& g, const DeviceTables& t, hipStream_t 
 hipError_t launch_rs_encode_bitslice(const RsGeom& g, hipStream_t s);  // GF(2^8), n <= 128
 hipError_t launch_rs_encode_axis(const RsGeom& g, hipStream_t s);       // GF(2^8), n <= 128
 hipError_t launch_rs_encode_axis_segs(const RsGeom* gs, uint32_t nseg, hipStream_t s);
+hipError_t launch_rs_encode_gf16x(const RsGeom& g, hipStream_t s);     // GF(2^16), n = 256 / 512
 // Full 2D extension of nsq squares: Q0 rows -> Q1, then all 2k columns -> Q2|Q3.
 // ods == nullptr means Q0 is already in place inside eds.
 hipError_t launch_extend(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t nsq,

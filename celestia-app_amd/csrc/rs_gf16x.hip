@@ -1,0 +1,436 @@
+// Leopard GF(2^16) encode (k = 256, 512: 2k > 256 shards), one wave per
+// (square, axis, 64-byte column), no LDS, no barrier.
+//
+// Replaces klauspost/reedsolomon v1.12.1 leopard.go Encode as rsmt2d v0.14.0's
+// LeoRSCodec drives it for more than 256 shards (pkg/appconsts/global_consts.go:92;
+// SURVEY.md Appendix A.3): IFFT of the K data shards over the coset at K, then FFT over
+// the coset at 0, radix 2 (the transform of rs_kernels.hip's header).
+//
+// Layout. A wave holds one 64-byte Leopard block (32 symbols) of every one of the K
+// shards of an axis in VGPRs: lane l = j + 8L takes dword j of the lo half and dword j
+// of the hi half of the block (4 symbols), so 8 lanes cover a block and L (3 bits) is
+// part of the shard index; each lane holds NR = K/8 shards, 2 dwords each (K = 512:
+// 128 VGPRs). Waves never talk to each other; 3 per SIMD overlap memory with compute.
+//
+// Arithmetic (gf16_constexpr.hpp). Symbols are kept in (a, b) coordinates over GF(2^8):
+// y = a + b*gamma. Every twiddle's representation is its block base >> layer, so every
+// twiddle is known from indices alone, and all but the lowest layers' twiddles lie in
+// the subfield GF(2^8), where a butterfly is a GF(2^8) butterfly on each byte.
+//
+// Two arrangements of the shard index s (K = 512; K = 256 drops bit 8):
+//   A: register r bits 0-4 = s bits 0-4, r bit 5 = s bit 8, lane L = s bits 5-7.
+//      Layers 0-4 (IFFT up, FFT down). Twiddle = compile-time part (register bits) XOR
+//      L << (5 - layer) (lane part, in GF(2^8)): v_perm product tables per lane, built
+//      by XORing the compile-time table with the lane's table of the layer.
+//   B: register r bits 0-1 = s bits 0-1, r bits 2.. = s bits 5.., lane L = s bits 2-4.
+//      Layers 5..log2(K)-1 have compile-time twiddles in GF(2^8): four shards x 4
+//      symbols x (a, b) = 32 bytes share every twiddle, so each 8-dword block is turned
+//      into 8 bit planes (8x8 bit transpose) and a butterfly is 8 xors plus an 8x8 GF(2)
+//      matrix network of xor3 ops.
+//   A <-> B swaps register bits 2, 3, 4 with lane bits 3, 4, 5: DPP row_ror:8,
+//   v_permlane16_swap and v_permlane32_swap (a 2x2 transpose per register pair each).
+#include <hip/hip_runtime.h>
+
+#include "bitslice8.hpp"
+#include "cel_internal.hpp"
+#include "gf16_constexpr.hpp"
+#include "gf8_constexpr.hpp"
+
+namespace cel {
+namespace g16 {
+
+using bs::pxor;
+using bs::tr8;
+using bs::xrow;
+using cx::sfor;
+using namespace g16c;
+
+// Constants materialised where used (volatile: keeps the compiler from hoisting every
+// twiddle's table into registers live across the transform). A VOP3 reads one SGPR.
+template <uint32_t C>
+__device__ __forceinline__ uint32_t sconst() {
+  uint32_t r;
+  asm volatile("s_mov_b32 %0, %1" : "=s"(r) : "i"(C));
+  return r;
+}
+template <uint32_t C>
+__device__ __forceinline__ uint32_t vconst() {
+  uint32_t r;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "i"(C));
+  return r;
+}
+__device__ __forceinline__ void pin(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d) {
+  asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+}
+
+// 3+3+2-bit selector fields of the 4 bytes of y (m7 = 0x07070707, m3 = 0x03030303).
+struct Sel {
+  uint32_t f0, f1, f2;
+};
+__device__ __forceinline__ Sel sel(uint32_t y, uint32_t m7, uint32_t m3) { return {y & m7, (y >> 3) & m7, (y >> 6) & m3}; }
+
+// A product table in registers (VGPR or SGPR operands).
+struct Tb {
+  uint32_t t0l, t0h, t1l, t1h, t2;
+};
+// x ^= the 4 byte products of the selectors by the table
+__device__ __forceinline__ uint32_t madd(uint32_t x, const Sel& s, const Tb& t) {
+  const uint32_t p0 = __builtin_amdgcn_perm(t.t0h, t.t0l, s.f0);
+  const uint32_t p1 = __builtin_amdgcn_perm(t.t1h, t.t1l, s.f1);
+  const uint32_t p2 = __builtin_amdgcn_perm(0u, t.t2, s.f2);
+  return __builtin_amdgcn_bitop3_b32(x, p0, p1, 0x96) ^ p2;
+}
+__device__ __forceinline__ uint32_t madd2(uint32_t x, const Sel& s, const Tb& t, const Sel& u, const Tb& v) {
+  const uint32_t p0 = __builtin_amdgcn_perm(t.t0h, t.t0l, s.f0);
+  const uint32_t p1 = __builtin_amdgcn_perm(t.t1h, t.t1l, s.f1);
+  const uint32_t p2 = __builtin_amdgcn_perm(0u, t.t2, s.f2);
+  const uint32_t q0 = __builtin_amdgcn_perm(v.t0h, v.t0l, u.f0);
+  const uint32_t q1 = __builtin_amdgcn_perm(v.t1h, v.t1l, u.f1);
+  const uint32_t q2 = __builtin_amdgcn_perm(0u, v.t2, u.f2);
+  return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(x, p0, p1, 0x96), __builtin_amdgcn_bitop3_b32(p2, q0, q1, 0x96),
+                                     q2, 0x96);
+}
+
+// Compile-time table of "multiply by C" (C < 256): high halves in SGPRs, low in VGPRs.
+template <uint32_t C>
+__device__ __forceinline__ Tb ctab() {
+  constexpr Tab8 t = tab8(C);
+  return Tb{vconst<t.t0l>(), sconst<t.t0h>(), vconst<t.t1l>(), sconst<t.t1h>(), sconst<t.t2>()};
+}
+// An opaque copy: values derived from it are computed where it is taken, not hoisted
+// to the top of the transform (every group's table would otherwise be built up front
+// and held in VGPRs).
+__device__ __forceinline__ Tb here(const Tb& g) {
+  Tb t = g;
+  asm volatile("" : "+v"(t.t0l), "+v"(t.t0h), "+v"(t.t1l), "+v"(t.t1h), "+v"(t.t2));
+  return t;
+}
+// Per-lane table: compile-time table of C XOR the lane's table g.
+template <uint32_t C>
+__device__ __forceinline__ Tb rtab(const Tb& g0) {
+  const Tb g = here(g0);
+  if constexpr (C == 0) {
+    return g;
+  } else {
+    constexpr Tab8 t = tab8(C);
+    return Tb{g.t0l ^ t.t0l, g.t0h ^ t.t0h, g.t1l ^ t.t1l, g.t1h ^ t.t1h, g.t2 ^ t.t2};
+  }
+}
+
+// The lane's table of c_g = L << S (S = 5 - layer): linear in c, so the XOR of the tables
+// of the bits of L, each selected by a lane mask (all ones where bit i of L is set).
+template <int S>
+__device__ __forceinline__ Tb lane_tab(uint32_t m0, uint32_t m1, uint32_t m2) {
+  constexpr Tab8 a = tab8(1u << S), b = tab8(2u << S), c = tab8(4u << S);
+  asm volatile("" : "+v"(m0), "+v"(m1), "+v"(m2));  // built where the layer starts
+  auto f = [&](uint32_t x, uint32_t y, uint32_t z) {
+    return (m0 & x) ^ (m1 & y) ^ (m2 & z);
+  };
+  return Tb{f(a.t0l, b.t0l, c.t0l), f(a.t0h, b.t0h, c.t0h), f(a.t1l, b.t1l, c.t1l), f(a.t1h, b.t1h, c.t1h),
+            f(a.t2, b.t2, c.t2)};
+}
+
+// Register index r (arrangement A) -> the register-held bits of the shard index.
+template <int LOGK>
+constexpr uint32_t shard_bits_a(uint32_t r) {
+  return (r & 31u) | ((r >> 5) << 8);
+}
+
+// One radix-2 layer of arrangement A (layer D_LOG in 0..4) over w[2r] (a), w[2r+1] (b).
+template <int LOGK, int D_LOG, bool IFFT, int NW>
+__device__ __forceinline__ void layer_a(uint32_t (&w)[NW], const Tb& g, uint32_t m7, uint32_t m3) {
+  constexpr uint32_t K = 1u << LOGK;
+  constexpr int NR = NW / 2;
+  constexpr int D = 1 << D_LOG;
+  sfor<NR / (2 * D)>([&](auto gi) {
+    // group base register: bit D_LOG clear, bits below zero
+    constexpr int blo = (decltype(gi)::value * 2 * D) & 31;
+    constexpr int bhi = ((decltype(gi)::value * 2 * D) >> 5) << 5;
+    constexpr int r0 = bhi | blo;
+    constexpr uint32_t base = shard_bits_a<LOGK>((uint32_t)r0);
+    constexpr uint32_t c = IFFT ? ifft_tw(K, D_LOG, base) : fft_tw(D_LOG, base);  // lane part added per lane
+    constexpr uint32_t ca = coord_a(c), cb = coord_b(c);
+    if constexpr (cb == 0) {
+      const Tb t = rtab<ca>(g);
+      sfor<D>([&](auto ji) {
+        constexpr int x = r0 + decltype(ji)::value, y = x + D;
+        pin(w[2 * x], w[2 * x + 1], w[2 * y], w[2 * y + 1]);
+        if constexpr (IFFT) {
+          w[2 * y] ^= w[2 * x];
+          w[2 * y + 1] ^= w[2 * x + 1];
+          w[2 * x] = madd(w[2 * x], sel(w[2 * y], m7, m3), t);
+          w[2 * x + 1] = madd(w[2 * x + 1], sel(w[2 * y + 1], m7, m3), t);
+        } else {
+          w[2 * x] = madd(w[2 * x], sel(w[2 * y], m7, m3), t);
+          w[2 * x + 1] = madd(w[2 * x + 1], sel(w[2 * y + 1], m7, m3), t);
+          w[2 * y] ^= w[2 * x];
+          w[2 * y + 1] ^= w[2 * x + 1];
+        }
+        pin(w[2 * x], w[2 * x + 1], w[2 * y], w[2 * y + 1]);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    } else {
+      // c = ca + cb*gamma (cb compile-time, ca = compile-time part ^ lane part):
+      //   x_a ^= ca*y_a + (cb p)*y_b,  x_b ^= cb*y_a + (ca + cb q)*y_b
+      const Tb tca = rtab<ca>(g);
+      const Tb tq = rtab<ca ^ mul(cb, kQ)>(g);
+      const Tb tcbp = ctab<mul(cb, kP)>();
+      const Tb tcb = ctab<cb>();
+      sfor<D>([&](auto ji) {
+        constexpr int x = r0 + decltype(ji)::value, y = x + D;
+        pin(w[2 * x], w[2 * x + 1], w[2 * y], w[2 * y + 1]);
+        if constexpr (IFFT) {
+          w[2 * y] ^= w[2 * x];
+          w[2 * y + 1] ^= w[2 * x + 1];
+        }
+        const Sel sa = sel(w[2 * y], m7, m3), sb = sel(w[2 * y + 1], m7, m3);
+        w[2 * x] = madd2(w[2 * x], sa, tca, sb, tcbp);
+        w[2 * x + 1] = madd2(w[2 * x + 1], sa, tcb, sb, tq);
+        if constexpr (!IFFT) {
+          w[2 * y] ^= w[2 * x];
+          w[2 * y + 1] ^= w[2 * x + 1];
+        }
+        pin(w[2 * x], w[2 * x + 1], w[2 * y], w[2 * y + 1]);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    }
+  });
+}
+
+// Register bit RB (2, 3, 4) <-> lane bit RB + 1 (8, 16, 32 lanes apart): a 2x2 transpose
+// of every register pair (r, r | 1 << RB), for both coordinates. An involution.
+template <int RB, int NW>
+__device__ __forceinline__ void swap_bit(uint32_t (&w)[NW]) {
+  constexpr int NR = NW / 2;
+  sfor<NR>([&](auto ri) {
+    constexpr int r = decltype(ri)::value;
+    if constexpr (!((r >> RB) & 1)) {
+      constexpr int r1 = r | (1 << RB);
+      sfor<2>([&](auto ci) {
+        constexpr int u = 2 * r + decltype(ci)::value, v = 2 * r1 + decltype(ci)::value;
+        if constexpr (RB == 4) {
+          const auto p = __builtin_amdgcn_permlane32_swap(w[u], w[v], false, false);
+          w[u] = p[0];
+          w[v] = p[1];
+        } else if constexpr (RB == 3) {
+          const auto p = __builtin_amdgcn_permlane16_swap(w[u], w[v], false, false);
+          w[u] = p[0];
+          w[v] = p[1];
+        } else {
+          // row_ror:8 reads lane l ^ 8; banks 2-3 (lane bit 3 set) take the partner's w[v]
+          // into w[u], banks 0-1 the partner's w[u] into w[v]
+          const uint32_t nu = __builtin_amdgcn_update_dpp(w[u], w[v], 0x128, 0xF, 0xC, false);
+          const uint32_t nv = __builtin_amdgcn_update_dpp(w[v], w[u], 0x128, 0xF, 0x3, false);
+          w[u] = nu;
+          w[v] = nv;
+        }
+      });
+    }
+  });
+}
+
+// planes w[XO..XO+8) ^= C * planes w[YO..YO+8) (C < 256; C == 0 adds nothing)
+template <uint32_t C, int XO, int YO, int NW>
+__device__ __forceinline__ void pmuladd(uint32_t (&w)[NW]) {
+  if constexpr (C != 0) {
+    sfor<8>([&](auto r) { xrow<mul_row8(C, decltype(r)::value), YO, 0>(w[XO + decltype(r)::value], w); });
+  }
+}
+
+// Arrangement B: block b = registers 4b..4b+3 = w[8b..8b+8), shard bits 5.. = b.
+template <int LOGK, int NW>
+__device__ __forceinline__ void stage_b(uint32_t (&w)[NW]) {
+  constexpr uint32_t K = 1u << LOGK;
+  constexpr int NB = NW / 8;
+  sfor<NB>([&](auto b) {
+    tr8<8 * decltype(b)::value>(w);
+    __builtin_amdgcn_sched_barrier(0);
+  });
+  // IFFT layers 5 .. LOGK-2
+  sfor<LOGK - 6>([&](auto t) {
+    constexpr int d = 5 + decltype(t)::value;
+    constexpr int DB = 1 << (d - 5);  // block distance
+    sfor<NB / (2 * DB)>([&](auto gi) {
+      constexpr int b0 = decltype(gi)::value * 2 * DB;
+      constexpr uint32_t c = ifft_tw(K, d, (uint32_t)b0 << 5);
+      sfor<DB>([&](auto ji) {
+        constexpr int x = 8 * (b0 + decltype(ji)::value), y = x + 8 * DB;
+        pxor<x, y>(w);
+        pmuladd<c, x, y>(w);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    });
+  });
+  {  // last IFFT layer and first FFT layer act on the same pairs: one multiply by c1 + c2
+    constexpr int d = LOGK - 1;
+    constexpr int DB = 1 << (d - 5);
+    constexpr uint32_t c = ifft_tw(K, d, 0) ^ fft_tw(d, 0);
+    sfor<DB>([&](auto ji) {
+      constexpr int x = 8 * decltype(ji)::value, y = x + 8 * DB;
+      pxor<x, y>(w);
+      pmuladd<c, x, y>(w);
+      pxor<x, y>(w);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  }
+  // FFT layers LOGK-2 .. 5
+  sfor<LOGK - 6>([&](auto t) {
+    constexpr int d = LOGK - 2 - decltype(t)::value;
+    constexpr int DB = 1 << (d - 5);
+    sfor<NB / (2 * DB)>([&](auto gi) {
+      constexpr int b0 = decltype(gi)::value * 2 * DB;
+      constexpr uint32_t c = fft_tw(d, (uint32_t)b0 << 5);
+      sfor<DB>([&](auto ji) {
+        constexpr int x = 8 * (b0 + decltype(ji)::value), y = x + 8 * DB;
+        pmuladd<c, x, y>(w);
+        pxor<x, y>(w);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    });
+  });
+  sfor<NB>([&](auto b) {
+    tr8<8 * decltype(b)::value>(w);
+    __builtin_amdgcn_sched_barrier(0);
+  });
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+
+// (lo, hi) -> (a, b): a = lo ^ A(hi), b = hi; the inverse is the same map. One table
+// materialisation for the whole array, one register's conversion at a time.
+template <int NW>
+__device__ __forceinline__ void convert(uint32_t (&w)[NW], uint32_t m7, uint32_t m3) {
+  constexpr Tab8 t = tab_amap();
+  const Tb tb{vconst<t.t0l>(), sconst<t.t0h>(), vconst<t.t1l>(), sconst<t.t1h>(), sconst<t.t2>()};
+  sfor<NW / 2>([&](auto ri) {
+    constexpr int i = decltype(ri)::value;
+    w[2 * i] = madd(w[2 * i], sel(w[2 * i + 1], m7, m3), tb);
+    __builtin_amdgcn_sched_barrier(0);
+  });
+}
+
+// Tile = (square z, axis x, 64-byte column cb): one wave. Shard j of the axis sits at
+// in + z*in_sq + x*in_axis + place(j) + 64*cb (see RsGeom; blocked placement for the
+// output and the data copy when blk_log != 0).
+template <int LOGK>
+__global__ __launch_bounds__(256, LOGK == 9 ? 2 : 4) void k_rs_gf16x(RsGeom g) {
+  constexpr int K = 1 << LOGK;
+  constexpr int NR = K / 8;
+  constexpr int NW = 2 * NR;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t tile = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+  const uint32_t nblk = g.len / 64u;
+  if (tile >= (uint32_t)g.axes * nblk * g.nsq) return;
+  const uint32_t cb = tile % nblk, r = tile / nblk;
+  const uint32_t x = r % g.axes, z = r / g.axes;
+  const uint32_t j = lane & 7u, L = lane >> 3;
+  const uint32_t col = cb * 64u + j * 4u;
+  const uint32_t m7 = sconst<0x07070707u>(), m3 = sconst<0x03030303u>();
+  const uint32_t blk_mask = g.blk_log ? (1u << g.blk_log) - 1u : 0xFFFFFFFFu;
+  const uint32_t blk_shift = g.blk_log ? g.blk_log : 31u;
+  // Shard index in arrangement A = a register part (register bits 0-4 -> shard bits 0-4,
+  // bit 5 -> shard bit 8) plus a lane part (L -> shard bits 5-7). The two occupy disjoint
+  // bits, so every placement below (linear or blocked) is the sum of a wave-uniform
+  // register term (the buffer instruction's SGPR offset) and a lane term (its VGPR
+  // offset): no per-register address VGPRs.
+  // (the shift and mask go through an opaque copy at each use site: otherwise the data
+  // copy's and the output's offsets share their scalar subterms, which stay live across
+  // the whole transform and spill)
+  auto place = [&](uint32_t s, uint32_t shard, uint32_t blk) {
+    uint32_t sh = blk_shift, mk = blk_mask;
+    asm volatile("" : "+s"(sh), "+s"(mk));
+    return (s >> sh) * blk + (s & mk) * shard;
+  };
+  auto reg_bits = [](uint32_t i) { return (i & 31u) | ((i >> 5) << 8); };
+  const uint32_t lane_bits = L << 5;
+  uint32_t w[NW];
+  {
+    const auto rin = rsrc(g.in + (uint64_t)z * g.in_sq + (uint64_t)x * g.in_axis);
+    const uint32_t in_shard = (uint32_t)g.in_shard;
+    const uint32_t vin = lane_bits * in_shard + col;
+#pragma unroll
+    for (int i = 0; i < NR; i++) {
+      const uint32_t so = __builtin_amdgcn_readfirstlane(reg_bits((uint32_t)i) * in_shard);
+      w[2 * i] = __builtin_amdgcn_raw_buffer_load_b32(rin, vin, so, 2);
+      w[2 * i + 1] = __builtin_amdgcn_raw_buffer_load_b32(rin, vin + 32u, so, 2);
+    }
+    if (g.dcopy) {
+      const auto rdc = rsrc(g.dcopy + (uint64_t)z * g.dc_sq + (uint64_t)x * g.dc_axis);
+      const uint32_t dc_shard = (uint32_t)g.dc_shard, dc_blk = (uint32_t)g.dc_blk;
+      const uint32_t vdc = place(lane_bits, dc_shard, dc_blk) + col;
+#pragma unroll
+      for (int i = 0; i < NR; i++) {
+        const uint32_t so = __builtin_amdgcn_readfirstlane(place(reg_bits((uint32_t)i), dc_shard, dc_blk));
+        __builtin_amdgcn_raw_buffer_store_b32(w[2 * i], rdc, vdc, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(w[2 * i + 1], rdc, vdc + 32u, so, 0);
+      }
+    }
+  }
+  convert(w, m7, m3);  // -> (a, b)
+  // lane masks of the bits of L
+  const uint32_t mk0 = (L & 1u) ? 0xFFFFFFFFu : 0u, mk1 = (L & 2u) ? 0xFFFFFFFFu : 0u,
+                 mk2 = (L & 4u) ? 0xFFFFFFFFu : 0u;
+  // IFFT, arrangement A
+  layer_a<LOGK, 0, true>(w, lane_tab<5>(mk0, mk1, mk2), m7, m3);
+  layer_a<LOGK, 1, true>(w, lane_tab<4>(mk0, mk1, mk2), m7, m3);
+  layer_a<LOGK, 2, true>(w, lane_tab<3>(mk0, mk1, mk2), m7, m3);
+  layer_a<LOGK, 3, true>(w, lane_tab<2>(mk0, mk1, mk2), m7, m3);
+  layer_a<LOGK, 4, true>(w, lane_tab<1>(mk0, mk1, mk2), m7, m3);
+  swap_bit<2>(w);
+  swap_bit<3>(w);
+  swap_bit<4>(w);
+  stage_b<LOGK>(w);
+  swap_bit<2>(w);
+  swap_bit<3>(w);
+  swap_bit<4>(w);
+  // FFT, arrangement A
+  layer_a<LOGK, 4, false>(w, lane_tab<1>(mk0, mk1, mk2), m7, m3);
+  layer_a<LOGK, 3, false>(w, lane_tab<2>(mk0, mk1, mk2), m7, m3);
+  layer_a<LOGK, 2, false>(w, lane_tab<3>(mk0, mk1, mk2), m7, m3);
+  layer_a<LOGK, 1, false>(w, lane_tab<4>(mk0, mk1, mk2), m7, m3);
+  layer_a<LOGK, 0, false>(w, lane_tab<5>(mk0, mk1, mk2), m7, m3);
+  convert(w, m7, m3);  // -> (lo, hi)
+  const auto rout = rsrc(g.out + (uint64_t)z * g.out_sq + (uint64_t)x * g.out_axis);
+  const uint32_t out_shard = (uint32_t)g.out_shard, out_blk = (uint32_t)g.out_blk;
+  const uint32_t vout = place(lane_bits, out_shard, out_blk) + col;
+#pragma unroll
+  for (int i = 0; i < NR; i++) {
+    const uint32_t so = __builtin_amdgcn_readfirstlane(place(reg_bits((uint32_t)i), out_shard, out_blk));
+    __builtin_amdgcn_raw_buffer_store_b32(w[2 * i], rout, vout, so, 2);
+    __builtin_amdgcn_raw_buffer_store_b32(w[2 * i + 1], rout, vout + 32u, so, 2);
+  }
+}
+
+template <int LOGK>
+static hipError_t launch(const RsGeom& g, hipStream_t s) {
+  const uint64_t tiles = (uint64_t)g.axes * (g.len / 64u) * g.nsq;
+  if (tiles == 0) return hipSuccess;
+  if (tiles > 0xFFFFFFF0ull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_rs_gf16x<LOGK>, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, s, g);
+  return hipGetLastError();
+}
+
+}  // namespace g16
+
+// Byte offsets must fit the 32-bit buffer offsets.
+static bool gf16x_geom_ok(const RsGeom& g) {
+  auto span = [&](uint64_t shard, uint64_t blk) {
+    return g.blk_log ? ((uint64_t)(g.n >> g.blk_log) * blk + (uint64_t)(1u << g.blk_log) * shard + g.len)
+                     : (uint64_t)g.n * shard + g.len;
+  };
+  return g.len % 64 == 0 && g.len > 0 && (uint64_t)g.n * g.in_shard + g.len < 0x7fffffffull &&
+         span(g.out_shard, g.out_blk) < 0x7fffffffull && (!g.dcopy || span(g.dc_shard, g.dc_blk) < 0x7fffffffull);
+}
+
+hipError_t launch_rs_encode_gf16x(const RsGeom& g, hipStream_t s) {
+  if (!gf16x_geom_ok(g)) return hipErrorInvalidValue;
+  switch (g.n) {
+    case 256: return g16::launch<8>(g, s);
+    case 512: return g16::launch<9>(g, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace cel

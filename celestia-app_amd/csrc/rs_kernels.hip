@@ -743,8 +743,7 @@ hipError_t launch_rs_encode(const RsGeom& g, const DeviceTables& t, hipStream_t 
       return e && std::string(e) == "lds";
     }();
     const bool reg = !lds_only || g.blk_log;
-    if (reg && g.n == 256 && g.len % 512 == 0) return launch_gf16p<8>(g, t, s);
-    if (reg && g.n == 512 && g.len % 512 == 0) return launch_gf16p<9>(g, t, s);
+    if (reg && (g.n == 256 || g.n == 512) && g.len % 64 == 0) return launch_rs_encode_gf16x(g, s);
     dim3 grid(g.axes, g.len / 64, g.nsq);
     const size_t lds = (size_t)g.n * 64;
     if (lds > 64 * 1024)

@@ -194,7 +194,7 @@ def test_dah_validate_basic_cases(ctx):
 
 
 @pytest.mark.parametrize("inplace", [True, False])
-@pytest.mark.parametrize("k,n", [(32, 5), (64, 3), (128, 13)])
+@pytest.mark.parametrize("k,n", [(32, 5), (64, 3), (128, 13), (256, 2)])
 def test_device_batch(ctx, oracle, k, n, inplace):
     """Device-resident batch (cel_dev_*). inplace: the ODS placed in Q0 of each EDS
     buffer by cel_dev_place_ods and extended in place (d_ods = NULL, the bench's input
