@@ -98,9 +98,6 @@ cel_status cel_ctx_create(int device, cel_ctx** out) {
     e = hipEventCreateWithFlags(&ctx->ev_done[i], hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_rs[i], hipEventDisableTiming);
   }
-  for (int i = 0; i <= cel_ctx::kChunks && e == hipSuccess; i++) {
-    e = hipEventCreateWithFlags(&ctx->ev_rows[i], hipEventDisableTiming);
-  }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_start, hipEventDisableTiming);
   if (e == hipSuccess) e = upload_tables(&ctx->tables);
   if (e != hipSuccess) {
@@ -124,9 +121,6 @@ void cel_ctx_destroy(cel_ctx* ctx) {
     for (int i = 0; i < cel_ctx::kChunks; i++) {
       if (ctx->ev_done[i]) (void)hipEventDestroy(ctx->ev_done[i]);
       if (ctx->ev_rs[i]) (void)hipEventDestroy(ctx->ev_rs[i]);
-    }
-    for (int i = 0; i <= cel_ctx::kChunks; i++) {
-      if (ctx->ev_rows[i]) (void)hipEventDestroy(ctx->ev_rows[i]);
     }
     if (ctx->ev_start) (void)hipEventDestroy(ctx->ev_start);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -170,40 +164,19 @@ cel_status cel_device_name(cel_ctx* ctx, char* buf, size_t len) {
 // DAH on stream sub[c % kPipe]. Extensions are chained (chunk c+1's starts when chunk
 // c's ends) so each runs on the whole chip while earlier chunks hash: the VALU-bound
 // hashing of chunk c overlaps the extension of chunk c+1, and only the last chunk's
-// latency-bound tree top + DAH is exposed. CEL_PIPE_CHUNKS overrides the chunk count.
-static uint32_t pipe_chunks_default() {
-  static const uint32_t v = [] {
-    const char* e = getenv("CEL_PIPE_CHUNKS");
-    const int x = e ? atoi(e) : 2;
-    return (uint32_t)(x < 1 ? 1 : (x > cel_ctx::kChunks ? cel_ctx::kChunks : x));
-  }();
-  return v;
-}
-
-static bool pipe_stagger() {
-  static const bool v = [] {
-    const char* e = getenv("CEL_PIPE_STAGGER");
-    return e && atoi(e) != 0;
-  }();
-  return v;
-}
+// latency-bound tree top + DAH is exposed. Two chunks (profiles/r1g_pipe_chunks_ab.txt).
+constexpr uint32_t kPipeChunks = 2;
 
 static void pipe_plan(uint32_t n, uint32_t* chunk, uint32_t* nchunks) {
-  uint32_t nc = n < pipe_chunks_default() ? n : pipe_chunks_default();
+  uint32_t nc = n < kPipeChunks ? n : kPipeChunks;
   if (nc == 0) nc = 1;
   *chunk = (n + nc - 1) / nc;
   *nchunks = (n + *chunk - 1) / *chunk;
 }
 
-// Chunks of the host-buffer pipeline (CEL_HOST_CHUNKS, default 4).
-static uint32_t host_chunks() {
-  static const uint32_t v = [] {
-    const char* e = getenv("CEL_HOST_CHUNKS");
-    const int x = e ? atoi(e) : 4;
-    return (uint32_t)(x < 1 ? 1 : (x > cel_ctx::kChunks ? cel_ctx::kChunks : x));
-  }();
-  return v;
-}
+// Chunks of the host-buffer pipeline: the upload of chunk c + 1, the compute of chunk c
+// and the copy-back of chunk c - 1 overlap (profiles/r1c_host_io.txt).
+constexpr uint32_t kHostChunks = 4;
 
 void* cel_host_alloc(size_t bytes) {
   void* p = nullptr;
@@ -256,13 +229,8 @@ cel_status cel_dev_extend_only(cel_ctx* ctx, const void* d_ods, uint32_t n, uint
   cel_status st = validate_square(ctx, k, kShare);
   if (st) return st;
   DeviceGuard g(ctx->device);
-  const uint32_t m = extend_overlap_chunks();
-  hipStream_t us = pick_stream(ctx, stream);
-  hipError_t e = m ? launch_extend_2s(static_cast<const uint8_t*>(d_ods), static_cast<uint8_t*>(d_eds), k, n,
-                                      std::min<uint32_t>(m, cel_ctx::kChunks), ctx->tables, us,
-                                      ctx->sub[us == ctx->sub[0] ? 1 : 0], ctx->ev_rows)
-                   : launch_extend(static_cast<const uint8_t*>(d_ods), static_cast<uint8_t*>(d_eds), k, n,
-                                   ctx->tables, us);
+  const hipError_t e = launch_extend(static_cast<const uint8_t*>(d_ods), static_cast<uint8_t*>(d_eds), k, n,
+                                     ctx->tables, pick_stream(ctx, stream));
   return e == hipSuccess ? CEL_OK : hip_fail(ctx, e, "extend");
 }
 
@@ -298,7 +266,6 @@ cel_status cel_dev_extend_batch(cel_ctx* ctx, const void* d_ods, uint32_t n, uin
     const uint32_t first = c * chunk, cnt = (first + chunk <= n) ? chunk : n - first;
     hipStream_t s = ctx->sub[c % cel_ctx::kPipe];
     if ((e = hipStreamWaitEvent(s, ctx->ev_start, 0)) != hipSuccess) break;
-    if (c > 0 && pipe_stagger() && (e = hipStreamWaitEvent(s, ctx->ev_rs[c - 1], 0)) != hipSuccess) break;
     const uint8_t* ods = d_ods ? static_cast<const uint8_t*>(d_ods) + first * ods_sq : nullptr;
     uint8_t* eds = static_cast<uint8_t*>(d_eds) + first * eds_sq;
     if ((e = launch_extend(ods, eds, k, cnt, ctx->tables, s)) != hipSuccess) break;
@@ -331,7 +298,7 @@ cel_status cel_extend_batch(cel_ctx* ctx, const uint8_t* ods, uint32_t n, uint32
   // overlap the kernels and copies of the others (the copies dominate: 40 MiB of
   // PCIe traffic per k=128 square against ~50 us of kernels). Host buffers from
   // cel_host_alloc (pinned) make every copy asynchronous.
-  const uint32_t nc = std::min<uint32_t>(n, host_chunks());
+  const uint32_t nc = std::min<uint32_t>(n, kHostChunks);
   const uint32_t chunk = (n + nc - 1) / nc;
   const uint32_t nchunks = (n + chunk - 1) / chunk;
   const uint32_t nstreams = std::min<uint32_t>(nchunks, cel_ctx::kPipe);

@@ -43,46 +43,37 @@ struct RsGeom {
   uint32_t nsq;   // squares
 };
 
-// Several geometries of the same n in one launch (rs_axis.hip): tiles
-// [end[i-1], end[i]) belong to g[i].
-constexpr uint32_t kMaxSegs = 3;
-struct RsSegs {
-  RsGeom g[kMaxSegs];
-  uint32_t nslice[kMaxSegs];
-  uint32_t end[kMaxSegs];
-  uint32_t nseg;
-};
-
-constexpr uint32_t kTw16Words = 20;    // dwords of one GF(2^16) v_perm product table
-constexpr uint32_t kTw16Count = 4096;  // skew indices covered (2n - 1 < 4096 for n <= 2048)
-
 struct DeviceTables {
   uint32_t* tw8 = nullptr;     // [255][8] GF(2^8) twiddle product tables, indexed by skew index
-  uint32_t* tw16 = nullptr;    // [kTw16Count][kTw16Words] GF(2^16) product tables, by skew index
   uint16_t* exp16 = nullptr;   // [65536]
   uint16_t* log16 = nullptr;   // [65536]
   uint16_t* skew16 = nullptr;  // [65535]
   uint32_t* mul8 = nullptr;    // [256][8] GF(2^8) product tables indexed by log value (decoder)
 };
 
+// XCD-aware workgroup order. Workgroups are dealt round-robin over the 8 XCDs
+// (MI355X_MICROARCH.md, "Workgroup dispatch"), so workgroup b shares an L2 with b + 8.
+// Map them so that each XCD works through one contiguous range of logical ids: the
+// column passes then stream adjacent column blocks through each XCD's L2 channels instead
+// of one fixed residue of column offsets per XCD. A bijection of [0, nb) for any nb;
+// for speed only (nothing relies on where a workgroup runs).
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
+  const uint32_t q = nb >> 3, r = nb & 7u, x = b & 7u;
+  return x * q + (x < r ? x : r) + (b >> 3);
+}
+
 hipError_t upload_tables(DeviceTables* t);
 void free_tables(DeviceTables* t);
 
 // Kernel launchers (rs_kernels.hip / nmt_kernels.hip). All asynchronous on `s`.
 hipError_t launch_rs_encode(const RsGeom& g, const DeviceTables& t, hipStream_t s);
-hipError_t launch_rs_encode_bitslice(const RsGeom& g, hipStream_t s);  // GF(2^8), n <= 128
-hipError_t launch_rs_encode_axis(const RsGeom& g, hipStream_t s);       // GF(2^8), n <= 128
-hipError_t launch_rs_encode_axis_segs(const RsGeom* gs, uint32_t nseg, hipStream_t s);
+hipError_t launch_rs_encode_bitslice(const RsGeom& g, hipStream_t s);  // GF(2^8), n <= 16
+hipError_t launch_rs_encode_axis(const RsGeom& g, hipStream_t s);       // GF(2^8), 32 <= n <= 128
 hipError_t launch_rs_encode_gf16x(const RsGeom& g, hipStream_t s);     // GF(2^16), n = 256 / 512
 // Full 2D extension of nsq squares: Q0 rows -> Q1, then all 2k columns -> Q2|Q3.
 // ods == nullptr means Q0 is already in place inside eds.
 hipError_t launch_extend(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t nsq,
                          const DeviceTables& t, hipStream_t s);
-// The same extension as m chunks over two streams: rows(c + 1) runs beside cols(c)
-// (an HBM-bound launch beside a VALU-bound one). ev: m + 1 events. s0 ends joined.
-hipError_t launch_extend_2s(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t nsq, uint32_t m,
-                            const DeviceTables& t, hipStream_t s0, hipStream_t s1, hipEvent_t* ev);
-uint32_t extend_overlap_chunks();
 
 // NMT + DAH over resident EDSs. work: scratch of nmt_workspace_size(k, nsq) bytes.
 size_t nmt_workspace_size(uint32_t k, uint32_t nsq);
@@ -155,7 +146,6 @@ struct cel_ctx {
   hipEvent_t ev_start = nullptr;
   hipEvent_t ev_done[kChunks] = {};
   hipEvent_t ev_rs[kChunks] = {};
-  hipEvent_t ev_rows[kChunks + 1] = {};  // two-stream extension: rows(c) done / join
   std::mutex mu;
   cel::DeviceTables tables;
   std::string last_error;

@@ -1,7 +1,7 @@
-// Leopard GF(2^8) encode, one wave per axis slice (k <= 128).
+// Leopard GF(2^8) encode, one wave per axis slice (32 <= k <= 128).
 //
-// Same transform as k_rs_encode_gf8 (SURVEY.md Appendix A.2 in radix-2 form, see the
-// header of rs_kernels.hip), laid out so that nothing is shared between waves:
+// The transform of SURVEY.md Appendix A.2 in radix-2 form (see the header of
+// rs_kernels.hip), laid out so that nothing is shared between waves:
 //   - a wave owns one tile = (square, axis, 256-byte slice); lane l holds dword l of
 //     the slice of every one of the K data shards of the axis in VGPRs (K <= 128);
 //   - every radix-2 layer is lane-local, so there is no LDS image and no barrier: the
@@ -13,8 +13,6 @@
 // Multiply: the byte splits into 3+3+2 bits, each looked up with one v_perm_b32 in
 // an 8/8/4-entry product table (as rs_kernels.hip gf8_mul4).
 #include <hip/hip_runtime.h>
-
-#include <cstdlib>
 
 #include "cel_internal.hpp"
 #include "bitslice8.hpp"
@@ -114,59 +112,6 @@ __device__ __forceinline__ void pin(uint32_t& a, uint32_t& b) { asm volatile("" 
 constexpr uint32_t merged_lm(uint32_t s1, uint32_t s2) {
   const uint32_t c = (s1 == 255u ? 0u : (uint32_t)kGf8.exp[s1]) ^ (s2 == 255u ? 0u : (uint32_t)kGf8.exp[s2]);
   return c == 0u ? 255u : (uint32_t)kGf8.log[c];
-}
-
-template <int K>
-__device__ __forceinline__ void transform(uint32_t (&w)[K]) {
-  constexpr int LOGK = __builtin_ctz(K);
-  const uint32_t m7 = sconst<0x07070707u>(), m3 = sconst<0x03030303u>();
-  if constexpr (K == 1) {
-    return;
-  } else {
-  sfor<LOGK - 1>([&](auto lg) {
-    constexpr int D = 1 << decltype(lg)::value;
-    sfor<K / (2 * D)>([&](auto bi) {
-      constexpr int base = decltype(bi)::value * 2 * D;
-      const Mul<kGf8.skew[K - 1 + base + D]> m;
-      sfor<D>([&](auto j) {
-        constexpr int a = base + decltype(j)::value;
-        pin(w[a], w[a + D]);
-        w[a + D] ^= w[a];
-        m.muladd(w[a], w[a + D], m7, m3);
-        pin(w[a], w[a + D]);
-        __builtin_amdgcn_sched_barrier(0);
-      });
-    });
-  });
-  {
-    constexpr int D = K / 2;
-    const Mul<merged_lm(kGf8.skew[K - 1 + D], kGf8.skew[D - 1])> m;
-    sfor<D>([&](auto j) {
-      constexpr int a = decltype(j)::value;
-      pin(w[a], w[a + D]);
-      w[a + D] ^= w[a];
-      m.muladd(w[a], w[a + D], m7, m3);
-      w[a + D] ^= w[a];
-      pin(w[a], w[a + D]);
-      __builtin_amdgcn_sched_barrier(0);
-    });
-  }
-  sfor<LOGK - 1>([&](auto t) {
-    constexpr int D = K >> (decltype(t)::value + 2);
-    sfor<K / (2 * D)>([&](auto bi) {
-      constexpr int base = decltype(bi)::value * 2 * D;
-      const Mul<kGf8.skew[base + D - 1]> m;
-      sfor<D>([&](auto j) {
-        constexpr int a = base + decltype(j)::value;
-        pin(w[a], w[a + D]);
-        m.muladd(w[a], w[a + D], m7, m3);
-        w[a + D] ^= w[a];
-        pin(w[a], w[a + D]);
-        __builtin_amdgcn_sched_barrier(0);
-      });
-    });
-  });
-  }
 }
 
 // ---------------------------------------------------------------- hybrid transform
@@ -274,111 +219,54 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
 }
 
-// DBG (profiling only, CEL_RS_DEBUG): 1 = loads and stores without the transform,
-// 2 = the transform without global memory traffic.
-//
-// One launch covers up to kMaxSegs geometries (RsSegs) of the same n: tiles
-// [end[i-1], end[i]) belong to segment i. The extension pipeline (launch_extend_axis)
-// puts the last column pass of chunk c-1 and both Q0 passes of chunk c in one launch.
-template <int LOGK, int DBG, bool HYB, int LDA = 0, int STA = 0>
-__global__ __launch_bounds__(256, 3) void k_rs_axis_gf8(RsSegs sg) {
+// Tile = (square z, axis x, 256-byte slice y): one wave. Loads and stores are nt
+// (non-temporal): every byte is touched once per pass and a batch is far larger than the
+// Infinity Cache (k=128, 256 squares: 9.35 -> 9.00 us per square against the default
+// policy, profiles/r1d_rs_cache_policy_ab.txt).
+template <int LOGK>
+__global__ __launch_bounds__(256, 3) void k_rs_axis_gf8(RsGeom g, uint32_t nslice) {
   constexpr int K = 1 << LOGK;
   const uint32_t lane = threadIdx.x & 63;
-  uint32_t tile = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
-  if (tile >= sg.end[sg.nseg - 1]) return;
-  uint32_t si = 0;
-#pragma unroll
-  for (uint32_t i = 0; i + 1 < kMaxSegs; i++) si += (tile >= sg.end[i] && i + 1 < sg.nseg) ? 1u : 0u;
-  si = __builtin_amdgcn_readfirstlane(si);
-  if (si > 0) tile -= sg.end[si - 1];
-  // field-wise selects on the scalar unit (a dynamic index into the kernarg struct
-  // would copy it to scratch)
-  const RsGeom g = si == 0 ? sg.g[0] : (si == 1 ? sg.g[1] : sg.g[2]);
-  const uint32_t nslice = si == 0 ? sg.nslice[0] : (si == 1 ? sg.nslice[1] : sg.nslice[2]);
+  const uint32_t tile = __builtin_amdgcn_readfirstlane(xcd_block(blockIdx.x, gridDim.x) * 4u + (threadIdx.x >> 6));
+  if (tile >= g.axes * nslice * g.nsq) return;
   const uint32_t y = tile % nslice, r = tile / nslice;
   const uint32_t x = r % g.axes, z = r / g.axes;
   const uint32_t col = y * 256u + lane * 4u;
   const bool active = col < g.len;
   const uint32_t lo = active ? lane * 4u : 0u;  // inactive lanes load (and never store) dword 0
   uint32_t w[K];
-  if constexpr (DBG == 2) {
-#pragma unroll
-    for (int i = 0; i < K; i++) w[i] = (col * 2654435761u) ^ (uint32_t)i;
-  } else {
+  {
     const auto rin = rsrc(g.in + (uint64_t)z * g.in_sq + (uint64_t)x * g.in_axis + (uint64_t)y * 256u);
     const uint32_t in_shard = (uint32_t)g.in_shard;
 #pragma unroll
-    for (int i = 0; i < K; i++) w[i] = __builtin_amdgcn_raw_buffer_load_b32(rin, lo, (uint32_t)i * in_shard, LDA);
+    for (int i = 0; i < K; i++) w[i] = __builtin_amdgcn_raw_buffer_load_b32(rin, lo, (uint32_t)i * in_shard, 2);
     if (g.dcopy && active) {
       const auto rdc = rsrc(g.dcopy + (uint64_t)z * g.dc_sq + (uint64_t)x * g.dc_axis + (uint64_t)y * 256u);
       const uint32_t dc_shard = (uint32_t)g.dc_shard;
 #pragma unroll
-      for (int i = 0; i < K; i++) __builtin_amdgcn_raw_buffer_store_b32(w[i], rdc, lo, (uint32_t)i * dc_shard, STA);
+      for (int i = 0; i < K; i++) __builtin_amdgcn_raw_buffer_store_b32(w[i], rdc, lo, (uint32_t)i * dc_shard, 2);
     }
   }
-  if constexpr (DBG != 1) {
-    if constexpr (HYB) transform_hyb<K>(w);
-    else transform<K>(w);
-  }
-  if constexpr (DBG == 2) {
-    uint32_t acc = 0;
-#pragma unroll
-    for (int i = 0; i < K; i++) acc ^= w[i];
-    if (acc == (uint32_t)g.in_sq + 0x9E3779B9u) g.out[col] = (uint8_t)acc;  // keeps the transform alive
-  } else if (active) {
+  transform_hyb<K>(w);
+  if (active) {
     const auto rout = rsrc(g.out + (uint64_t)z * g.out_sq + (uint64_t)x * g.out_axis + (uint64_t)y * 256u);
     const uint32_t out_shard = (uint32_t)g.out_shard;
 #pragma unroll
-    for (int i = 0; i < K; i++) __builtin_amdgcn_raw_buffer_store_b32(w[i], rout, lo, (uint32_t)i * out_shard, STA);
+    for (int i = 0; i < K; i++) __builtin_amdgcn_raw_buffer_store_b32(w[i], rout, lo, (uint32_t)i * out_shard, 2);
   }
 }
 
-// Buffer cache-policy bits of the loads and stores. Default: nt (non-temporal) on both:
-// every byte is touched once per pass and the batch is far larger than the Infinity
-// Cache; k=128 B=256: 9.35 -> 9.00 us per square (profiles/r1d_rs_cache_policy_ab.txt).
-// CEL_RS_CP (A/B only): 0 default policy, 1 nt stores only, 3 sc0|sc1 stores.
-static int rs_cache_policy() {
-  static const int v = [] {
-    const char* e = getenv("CEL_RS_CP");
-    return e ? atoi(e) : 2;
-  }();
-  return v;
-}
-
-template <int LOGK, bool HYB>
-hipError_t launch(const RsSegs& sg, hipStream_t s, int dbg) {
-  const uint32_t ntiles = sg.end[sg.nseg - 1];
+template <int LOGK>
+hipError_t launch(const RsGeom& g, hipStream_t s) {
+  const uint32_t nslice = (g.len + 255) / 256;
+  const uint64_t ntiles = (uint64_t)g.axes * nslice * g.nsq;
   if (ntiles == 0) return hipSuccess;
-  const dim3 grid((ntiles + 3) / 4);
-  const int cp = rs_cache_policy();
-  if (dbg == 1) hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 1, false>), grid, dim3(256), 0, s, sg);
-  else if (dbg == 2) hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 2, HYB>), grid, dim3(256), 0, s, sg);
-  else if (cp == 0) hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 0, HYB>), grid, dim3(256), 0, s, sg);
-  else if (HYB && cp == 1) hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 0, HYB, 0, 2>), grid, dim3(256), 0, s, sg);
-  else if (HYB && cp == 3) hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 0, HYB, 0, 17>), grid, dim3(256), 0, s, sg);
-  else hipLaunchKernelGGL((k_rs_axis_gf8<LOGK, 0, HYB, 2, 2>), grid, dim3(256), 0, s, sg);
+  if (ntiles > 0xFFFFFFF0ull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_rs_axis_gf8<LOGK>, dim3((unsigned)((ntiles + 3) / 4)), dim3(256), 0, s, g, nslice);
   return hipGetLastError();
 }
 
 }  // namespace ax
-
-static int rs_debug() {
-  static const int dbg = [] {
-    const char* e = getenv("CEL_RS_DEBUG");
-    return e ? atoi(e) : 0;
-  }();
-  return dbg;
-}
-
-// Bit-sliced D >= 8 layers (transform_hyb) for n >= 32: CEL_RS_HYB=0 selects the
-// all-v_perm transform.
-static bool rs_hybrid() {
-  static const bool v = [] {
-    const char* e = getenv("CEL_RS_HYB");
-    return e ? atoi(e) != 0 : true;
-  }();
-  return v;
-}
 
 // Byte offsets must fit the 32-bit buffer offsets: (n - 1) * shard stride + len < 2 GiB.
 static bool geom_ok(const RsGeom& g) {
@@ -386,36 +274,15 @@ static bool geom_ok(const RsGeom& g) {
   return span < 0x7fffffffull && !(g.dcopy && (uint64_t)g.n * g.dc_shard + g.len >= 0x7fffffffull);
 }
 
-hipError_t launch_rs_encode_axis_segs(const RsGeom* gs, uint32_t nseg, hipStream_t s) {
-  if (nseg == 0 || nseg > kMaxSegs) return hipErrorInvalidValue;
-  RsSegs sg{};
-  uint64_t end = 0;
-  for (uint32_t i = 0; i < nseg; i++) {
-    const RsGeom& g = gs[i];
-    if (g.n != gs[0].n || !geom_ok(g) || g.len == 0) return hipErrorInvalidValue;
-    sg.g[i] = g;
-    sg.nslice[i] = (g.len + 255) / 256;
-    end += (uint64_t)g.axes * sg.nslice[i] * g.nsq;
-    if (end > 0xFFFFFFF0ull) return hipErrorInvalidValue;
-    sg.end[i] = (uint32_t)end;
-  }
-  sg.nseg = nseg;
-  const int dbg = rs_debug();
-  const bool hyb = rs_hybrid();
-  switch (gs[0].n) {
-    case 1: return ax::launch<0, false>(sg, s, dbg);
-    case 2: return ax::launch<1, false>(sg, s, dbg);
-    case 4: return ax::launch<2, false>(sg, s, dbg);
-    case 8: return ax::launch<3, false>(sg, s, dbg);
-    case 16: return ax::launch<4, false>(sg, s, dbg);
-    case 32: return hyb ? ax::launch<5, true>(sg, s, dbg) : ax::launch<5, false>(sg, s, dbg);
-    case 64: return hyb ? ax::launch<6, true>(sg, s, dbg) : ax::launch<6, false>(sg, s, dbg);
-    case 128: return hyb ? ax::launch<7, true>(sg, s, dbg) : ax::launch<7, false>(sg, s, dbg);
+hipError_t launch_rs_encode_axis(const RsGeom& g, hipStream_t s) {
+  if (!geom_ok(g) || g.len == 0) return hipErrorInvalidValue;
+  switch (g.n) {
+    case 32: return ax::launch<5>(g, s);
+    case 64: return ax::launch<6>(g, s);
+    case 128: return ax::launch<7>(g, s);
     default: return hipErrorInvalidValue;
   }
 }
-
-hipError_t launch_rs_encode_axis(const RsGeom& g, hipStream_t s) { return launch_rs_encode_axis_segs(&g, 1, s); }
 
 }  // namespace cel
 

@@ -97,24 +97,24 @@ __device__ __forceinline__ Tb ctab() {
   constexpr Tab8 t = tab8(C);
   return Tb{vconst<t.t0l>(), sconst<t.t0h>(), vconst<t.t1l>(), sconst<t.t1h>(), sconst<t.t2>()};
 }
-// An opaque copy: values derived from it are computed where it is taken, not hoisted
-// to the top of the transform (every group's table would otherwise be built up front
-// and held in VGPRs).
-__device__ __forceinline__ Tb here(const Tb& g) {
-  Tb t = g;
-  asm volatile("" : "+v"(t.t0l), "+v"(t.t0h), "+v"(t.t1l), "+v"(t.t1h), "+v"(t.t2));
-  return t;
+// x ^ C as one volatile instruction: each group's table is built where the group starts
+// (plain XORs would be hoisted to the top of the transform, or CSE'd between layers, and
+// held in VGPRs), straight from the layer's lane table, with no copy.
+template <uint32_t C>
+__device__ __forceinline__ uint32_t vxor(uint32_t v) {
+  if constexpr (C == 0) {
+    return v;
+  } else {
+    uint32_t r;
+    asm volatile("v_xor_b32 %0, %1, %2" : "=v"(r) : "i"(C), "v"(v));
+    return r;
+  }
 }
 // Per-lane table: compile-time table of C XOR the lane's table g.
 template <uint32_t C>
-__device__ __forceinline__ Tb rtab(const Tb& g0) {
-  const Tb g = here(g0);
-  if constexpr (C == 0) {
-    return g;
-  } else {
-    constexpr Tab8 t = tab8(C);
-    return Tb{g.t0l ^ t.t0l, g.t0h ^ t.t0h, g.t1l ^ t.t1l, g.t1h ^ t.t1h, g.t2 ^ t.t2};
-  }
+__device__ __forceinline__ Tb rtab(const Tb& g) {
+  constexpr Tab8 t = tab8(C);
+  return Tb{vxor<t.t0l>(g.t0l), vxor<t.t0h>(g.t0h), vxor<t.t1l>(g.t1l), vxor<t.t1h>(g.t1h), vxor<t.t2>(g.t2)};
 }
 
 // The lane's table of c_g = L << S (S = 5 - layer): linear in c, so the XOR of the tables
@@ -311,22 +311,46 @@ __device__ __forceinline__ void convert(uint32_t (&w)[NW], uint32_t m7, uint32_t
   });
 }
 
+typedef uint32_t D2 __attribute__((ext_vector_type(2)));
+
+// Memory <-> register layout. A wave moves a block with 8-byte accesses, 8 lanes per
+// shard (one 64-byte segment per shard per instruction: dword-wide accesses, 8 x 32-byte
+// segments per instruction, ran the column pass at 1.9 TB/s without any transform,
+// tools/microbench/gf16_mem.hip), so lane bit 2 first holds the lo/hi half of the block
+// and the two dwords of an access are neighbours in the half. One exchange across lane
+// bit 2 (a 2x2 transpose of every register pair, DPP row_ror:4 / row_ror:12 in alternate
+// 4-lane banks) turns each pair into (lo dword, hi dword) of the same 4 symbols and lane
+// bit 2 into a column bit; it is an involution, so the same exchange undoes it before
+// the stores.
+template <int NW>
+__device__ __forceinline__ void pair_lo_hi(uint32_t (&w)[NW]) {
+  sfor<NW / 2>([&](auto ri) {
+    constexpr int i = decltype(ri)::value;
+    // banks 1, 3 (lane bit 2 set) take the partner's second dword into the first;
+    // banks 0, 2 take the partner's first dword into the second
+    const uint32_t lo = __builtin_amdgcn_update_dpp(w[2 * i], w[2 * i + 1], 0x124, 0xF, 0xA, false);
+    const uint32_t hi = __builtin_amdgcn_update_dpp(w[2 * i + 1], w[2 * i], 0x12C, 0xF, 0x5, false);
+    w[2 * i] = lo;
+    w[2 * i + 1] = hi;
+  });
+}
+
 // Tile = (square z, axis x, 64-byte column cb): one wave. Shard j of the axis sits at
 // in + z*in_sq + x*in_axis + place(j) + 64*cb (see RsGeom; blocked placement for the
 // output and the data copy when blk_log != 0).
 template <int LOGK>
-__global__ __launch_bounds__(256, LOGK == 9 ? 2 : 4) void k_rs_gf16x(RsGeom g) {
+__global__ __launch_bounds__(256, LOGK == 9 ? 3 : 4) void k_rs_gf16x(RsGeom g) {
   constexpr int K = 1 << LOGK;
   constexpr int NR = K / 8;
   constexpr int NW = 2 * NR;
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t tile = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+  const uint32_t tile = __builtin_amdgcn_readfirstlane(xcd_block(blockIdx.x, gridDim.x) * 4u + (threadIdx.x >> 6));
   const uint32_t nblk = g.len / 64u;
   if (tile >= (uint32_t)g.axes * nblk * g.nsq) return;
   const uint32_t cb = tile % nblk, r = tile / nblk;
   const uint32_t x = r % g.axes, z = r / g.axes;
-  const uint32_t j = lane & 7u, L = lane >> 3;
-  const uint32_t col = cb * 64u + j * 4u;
+  const uint32_t L = lane >> 3;
+  const uint32_t col = cb * 64u + (lane & 7u) * 8u;  // 8 lanes x 8 B = one 64-byte block
   const uint32_t m7 = sconst<0x07070707u>(), m3 = sconst<0x03030303u>();
   const uint32_t blk_mask = g.blk_log ? (1u << g.blk_log) - 1u : 0xFFFFFFFFu;
   const uint32_t blk_shift = g.blk_log ? g.blk_log : 31u;
@@ -353,8 +377,9 @@ __global__ __launch_bounds__(256, LOGK == 9 ? 2 : 4) void k_rs_gf16x(RsGeom g) {
 #pragma unroll
     for (int i = 0; i < NR; i++) {
       const uint32_t so = __builtin_amdgcn_readfirstlane(reg_bits((uint32_t)i) * in_shard);
-      w[2 * i] = __builtin_amdgcn_raw_buffer_load_b32(rin, vin, so, 2);
-      w[2 * i + 1] = __builtin_amdgcn_raw_buffer_load_b32(rin, vin + 32u, so, 2);
+      const auto v = __builtin_amdgcn_raw_buffer_load_b64(rin, vin, so, 2);
+      w[2 * i] = v[0];
+      w[2 * i + 1] = v[1];
     }
     if (g.dcopy) {
       const auto rdc = rsrc(g.dcopy + (uint64_t)z * g.dc_sq + (uint64_t)x * g.dc_axis);
@@ -363,11 +388,11 @@ __global__ __launch_bounds__(256, LOGK == 9 ? 2 : 4) void k_rs_gf16x(RsGeom g) {
 #pragma unroll
       for (int i = 0; i < NR; i++) {
         const uint32_t so = __builtin_amdgcn_readfirstlane(place(reg_bits((uint32_t)i), dc_shard, dc_blk));
-        __builtin_amdgcn_raw_buffer_store_b32(w[2 * i], rdc, vdc, so, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(w[2 * i + 1], rdc, vdc + 32u, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(D2{w[2 * i], w[2 * i + 1]}, rdc, vdc, so, 0);
       }
     }
   }
+  pair_lo_hi(w);
   convert(w, m7, m3);  // -> (a, b)
   // lane masks of the bits of L
   const uint32_t mk0 = (L & 1u) ? 0xFFFFFFFFu : 0u, mk1 = (L & 2u) ? 0xFFFFFFFFu : 0u,
@@ -392,14 +417,14 @@ __global__ __launch_bounds__(256, LOGK == 9 ? 2 : 4) void k_rs_gf16x(RsGeom g) {
   layer_a<LOGK, 1, false>(w, lane_tab<4>(mk0, mk1, mk2), m7, m3);
   layer_a<LOGK, 0, false>(w, lane_tab<5>(mk0, mk1, mk2), m7, m3);
   convert(w, m7, m3);  // -> (lo, hi)
+  pair_lo_hi(w);
   const auto rout = rsrc(g.out + (uint64_t)z * g.out_sq + (uint64_t)x * g.out_axis);
   const uint32_t out_shard = (uint32_t)g.out_shard, out_blk = (uint32_t)g.out_blk;
   const uint32_t vout = place(lane_bits, out_shard, out_blk) + col;
 #pragma unroll
   for (int i = 0; i < NR; i++) {
     const uint32_t so = __builtin_amdgcn_readfirstlane(place(reg_bits((uint32_t)i), out_shard, out_blk));
-    __builtin_amdgcn_raw_buffer_store_b32(w[2 * i], rout, vout, so, 2);
-    __builtin_amdgcn_raw_buffer_store_b32(w[2 * i + 1], rout, vout + 32u, so, 2);
+    __builtin_amdgcn_raw_buffer_store_b64(D2{w[2 * i], w[2 * i + 1]}, rout, vout, so, 2);
   }
 }
 

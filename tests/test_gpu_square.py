@@ -200,8 +200,7 @@ def test_device_batch(ctx, oracle, k, n, inplace):
     buffer by cel_dev_place_ods and extended in place (d_ods = NULL, the bench's input
     layout); otherwise a separate ODS buffer whose rows the row pass copies into Q0.
     EDS bytes, roots and DAH against the oracle for every square; a second
-    extend_only over the same buffers is idempotent. (tools/gpu_pipe2.sh runs the
-    same test with CEL_RS_CHUNK=6: three chunks of the chunked schedule at (128, 13).)"""
+    extend_only over the same buffers is idempotent."""
     import ctypes
     from celestia_eds import _lib
     from hipmem import DeviceBuffer, synchronize

@@ -57,6 +57,5 @@ for _ in range(a.reps):
     once()
 dt = (time.perf_counter() - t0) / a.reps
 mode = ("ODS in, roots+DAH out" if a.no_eds else "ODS in, EDS+roots+DAH out") + (", pinned" if a.pinned else ", pageable")
-mode += f", CEL_HOST_CHUNKS={os.environ.get('CEL_HOST_CHUNKS', '4')}"
 print(f"host-buffer cel_extend_batch k={k} batch={n} ({mode}): {dt * 1e3:.2f} ms per call = "
       f"{n / dt:.0f} squares/s; bytes over PCIe {(ods.nbytes + (0 if eds is None else eds.nbytes)) / dt / 1e9:.1f} GB/s")
