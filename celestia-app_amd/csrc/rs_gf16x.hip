@@ -137,61 +137,74 @@ constexpr uint32_t shard_bits_a(uint32_t r) {
 }
 
 // One radix-2 layer of arrangement A (layer D_LOG in 0..4) over w[2r] (a), w[2r+1] (b).
+// Groups run in two halves by register bit 5 (shard bit 8): the twiddle's gamma
+// coordinate cb is constant over a half (it only sees shard bit 8 and K), so the
+// lane-independent tables of cb and cb*p are built once per half.
 template <int LOGK, int D_LOG, bool IFFT, int NW>
 __device__ __forceinline__ void layer_a(uint32_t (&w)[NW], const Tb& g, uint32_t m7, uint32_t m3) {
   constexpr uint32_t K = 1u << LOGK;
   constexpr int NR = NW / 2;
   constexpr int D = 1 << D_LOG;
-  sfor<NR / (2 * D)>([&](auto gi) {
-    // group base register: bit D_LOG clear, bits below zero
-    constexpr int blo = (decltype(gi)::value * 2 * D) & 31;
-    constexpr int bhi = ((decltype(gi)::value * 2 * D) >> 5) << 5;
-    constexpr int r0 = bhi | blo;
-    constexpr uint32_t base = shard_bits_a<LOGK>((uint32_t)r0);
-    constexpr uint32_t c = IFFT ? ifft_tw(K, D_LOG, base) : fft_tw(D_LOG, base);  // lane part added per lane
-    constexpr uint32_t ca = coord_a(c), cb = coord_b(c);
+  constexpr int NH = NR / 32;      // halves (1 for K = 256)
+  constexpr int GPH = 32 / (2 * D);  // groups per half
+  auto tw = [](int r0) constexpr { return IFFT ? ifft_tw(K, D_LOG, shard_bits_a<LOGK>((uint32_t)r0))
+                                               : fft_tw(D_LOG, shard_bits_a<LOGK>((uint32_t)r0)); };
+  sfor<NH>([&](auto hi) {
+    constexpr int h = decltype(hi)::value;
+    constexpr uint32_t cb = coord_b(tw(32 * h));
     if constexpr (cb == 0) {
-      const Tb t = rtab<ca>(g);
-      sfor<D>([&](auto ji) {
-        constexpr int x = r0 + decltype(ji)::value, y = x + D;
-        pin(w[2 * x], w[2 * x + 1], w[2 * y], w[2 * y + 1]);
-        if constexpr (IFFT) {
-          w[2 * y] ^= w[2 * x];
-          w[2 * y + 1] ^= w[2 * x + 1];
-          w[2 * x] = madd(w[2 * x], sel(w[2 * y], m7, m3), t);
-          w[2 * x + 1] = madd(w[2 * x + 1], sel(w[2 * y + 1], m7, m3), t);
-        } else {
-          w[2 * x] = madd(w[2 * x], sel(w[2 * y], m7, m3), t);
-          w[2 * x + 1] = madd(w[2 * x + 1], sel(w[2 * y + 1], m7, m3), t);
-          w[2 * y] ^= w[2 * x];
-          w[2 * y + 1] ^= w[2 * x + 1];
-        }
-        pin(w[2 * x], w[2 * x + 1], w[2 * y], w[2 * y + 1]);
-        __builtin_amdgcn_sched_barrier(0);
+      sfor<GPH>([&](auto gi) {
+        constexpr int r0 = 32 * h + decltype(gi)::value * 2 * D;  // bit D_LOG clear, bits below zero
+        constexpr uint32_t c = tw(r0);  // lane part added per lane
+        static_assert(coord_b(c) == cb, "gamma coordinate varies inside a half");
+        const Tb t = rtab<coord_a(c)>(g);
+        sfor<D>([&](auto ji) {
+          constexpr int x = r0 + decltype(ji)::value, y = x + D;
+          pin(w[2 * x], w[2 * x + 1], w[2 * y], w[2 * y + 1]);
+          if constexpr (IFFT) {
+            w[2 * y] ^= w[2 * x];
+            w[2 * y + 1] ^= w[2 * x + 1];
+            w[2 * x] = madd(w[2 * x], sel(w[2 * y], m7, m3), t);
+            w[2 * x + 1] = madd(w[2 * x + 1], sel(w[2 * y + 1], m7, m3), t);
+          } else {
+            w[2 * x] = madd(w[2 * x], sel(w[2 * y], m7, m3), t);
+            w[2 * x + 1] = madd(w[2 * x + 1], sel(w[2 * y + 1], m7, m3), t);
+            w[2 * y] ^= w[2 * x];
+            w[2 * y + 1] ^= w[2 * x + 1];
+          }
+          pin(w[2 * x], w[2 * x + 1], w[2 * y], w[2 * y + 1]);
+          __builtin_amdgcn_sched_barrier(0);
+        });
       });
     } else {
       // c = ca + cb*gamma (cb compile-time, ca = compile-time part ^ lane part):
       //   x_a ^= ca*y_a + (cb p)*y_b,  x_b ^= cb*y_a + (ca + cb q)*y_b
-      const Tb tca = rtab<ca>(g);
-      const Tb tq = rtab<ca ^ mul(cb, kQ)>(g);
       const Tb tcbp = ctab<mul(cb, kP)>();
       const Tb tcb = ctab<cb>();
-      sfor<D>([&](auto ji) {
-        constexpr int x = r0 + decltype(ji)::value, y = x + D;
-        pin(w[2 * x], w[2 * x + 1], w[2 * y], w[2 * y + 1]);
-        if constexpr (IFFT) {
-          w[2 * y] ^= w[2 * x];
-          w[2 * y + 1] ^= w[2 * x + 1];
-        }
-        const Sel sa = sel(w[2 * y], m7, m3), sb = sel(w[2 * y + 1], m7, m3);
-        w[2 * x] = madd2(w[2 * x], sa, tca, sb, tcbp);
-        w[2 * x + 1] = madd2(w[2 * x + 1], sa, tcb, sb, tq);
-        if constexpr (!IFFT) {
-          w[2 * y] ^= w[2 * x];
-          w[2 * y + 1] ^= w[2 * x + 1];
-        }
-        pin(w[2 * x], w[2 * x + 1], w[2 * y], w[2 * y + 1]);
-        __builtin_amdgcn_sched_barrier(0);
+      sfor<GPH>([&](auto gi) {
+        constexpr int r0 = 32 * h + decltype(gi)::value * 2 * D;
+        constexpr uint32_t c = tw(r0);
+        static_assert(coord_b(c) == cb, "gamma coordinate varies inside a half");
+        constexpr uint32_t ca = coord_a(c);
+        const Tb tca = rtab<ca>(g);
+        const Tb tq = rtab<ca ^ mul(cb, kQ)>(g);
+        sfor<D>([&](auto ji) {
+          constexpr int x = r0 + decltype(ji)::value, y = x + D;
+          pin(w[2 * x], w[2 * x + 1], w[2 * y], w[2 * y + 1]);
+          if constexpr (IFFT) {
+            w[2 * y] ^= w[2 * x];
+            w[2 * y + 1] ^= w[2 * x + 1];
+          }
+          const Sel sa = sel(w[2 * y], m7, m3), sb = sel(w[2 * y + 1], m7, m3);
+          w[2 * x] = madd2(w[2 * x], sa, tca, sb, tcbp);
+          w[2 * x + 1] = madd2(w[2 * x + 1], sa, tcb, sb, tq);
+          if constexpr (!IFFT) {
+            w[2 * y] ^= w[2 * x];
+            w[2 * y + 1] ^= w[2 * x + 1];
+          }
+          pin(w[2 * x], w[2 * x + 1], w[2 * y], w[2 * y + 1]);
+          __builtin_amdgcn_sched_barrier(0);
+        });
       });
     }
   });

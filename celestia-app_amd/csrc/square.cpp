@@ -96,14 +96,54 @@ static bool read_uvarint(const uint8_t*& p, const uint8_t* end, uint64_t& v) {
   return false;
 }
 
-// Decodes one message level; false on malformed wire data (proto.Unmarshal error).
+// Skips the rest of a group whose start key (wire type 3) was just read: nested fields up
+// to the matching end-group key. The generated gogoproto skip function (skipBlob) does the
+// same for unknown fields; false where it returns an error.
+static bool skip_group(const uint8_t*& p, const uint8_t* end) {
+  int depth = 1;
+  while (p < end) {
+    uint64_t key, v;
+    if (!read_uvarint(p, end, key)) return false;
+    switch (key & 7) {
+      case 0:
+        if (!read_uvarint(p, end, v)) return false;
+        break;
+      case 1:
+        if (end - p < 8) return false;
+        p += 8;
+        break;
+      case 2:
+        if (!read_uvarint(p, end, v) || v > (uint64_t)(end - p)) return false;
+        p += v;
+        break;
+      case 3:
+        depth++;
+        break;
+      case 4:
+        if (--depth == 0) return true;
+        break;
+      case 5:
+        if (end - p < 4) return false;
+        p += 4;
+        break;
+      default:
+        return false;
+    }
+  }
+  return false;
+}
+
+// Decodes one message level; false on malformed wire data (proto.Unmarshal error). The
+// field number is the key's bits 3.. taken as an int32, and must be > 0 (gogoproto
+// "illegal tag"); an end-group key outside a group is an error; a group (wire type 3) is
+// kept as a field of wire type 3 so that a known field number rejects it.
 static bool parse_fields(const uint8_t* p, size_t n, std::vector<Field>& out) {
   const uint8_t* end = p + n;
   while (p < end) {
     uint64_t key;
     if (!read_uvarint(p, end, key)) return false;
     Field f{(uint32_t)(key >> 3), (uint32_t)(key & 7), 0, nullptr, 0};
-    if (f.num == 0) return false;
+    if ((int32_t)f.num <= 0) return false;
     switch (f.wire) {
       case 0:
         if (!read_uvarint(p, end, f.varint)) return false;
@@ -122,6 +162,9 @@ static bool parse_fields(const uint8_t* p, size_t n, std::vector<Field>& out) {
         p += ln;
         break;
       }
+      case 3:
+        if (!skip_group(p, end)) return false;
+        break;
       case 5:
         if (end - p < 4) return false;
         f.p = p;

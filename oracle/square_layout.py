@@ -40,62 +40,119 @@ def uvarint(n: int) -> bytes:
             return bytes(out)
 
 
+class WireError(ValueError):
+    """proto.Unmarshal error (the gogoproto generated decoder's error cases)."""
+
+
 def _read_varint(buf, i):
-    shift = 0
+    """At most 10 bytes (shift < 64); the bits past 64 are dropped, as in Go."""
     val = 0
-    while True:
+    for shift in range(0, 64, 7):
+        if i >= len(buf):
+            raise WireError("unexpected EOF")
         b = buf[i]
         i += 1
         val |= (b & 0x7F) << shift
         if not b & 0x80:
-            return val, i
-        shift += 7
+            return val & (2**64 - 1), i
+    raise WireError("integer overflow")
+
+
+def _skip_group(buf, i):
+    """The rest of a group after its start key: nested fields up to the matching
+    end-group key (gogoproto skipBlob)."""
+    depth = 1
+    while i < len(buf):
+        key, i = _read_varint(buf, i)
+        wt = key & 7
+        if wt == 0:
+            _, i = _read_varint(buf, i)
+        elif wt == 1 or wt == 5:
+            i += 8 if wt == 1 else 4
+            if i > len(buf):
+                raise WireError("unexpected EOF")
+        elif wt == 2:
+            ln, i = _read_varint(buf, i)
+            if ln > len(buf) - i:
+                raise WireError("unexpected EOF")
+            i += ln
+        elif wt == 3:
+            depth += 1
+        elif wt == 4:
+            depth -= 1
+            if depth == 0:
+                return i
+        else:
+            raise WireError("illegal wire type")
+    raise WireError("unexpected EOF")
 
 
 def parse_proto(buf: bytes):
-    """Minimal protobuf wire decoder -> list of (field, wiretype, value)."""
+    """Protobuf wire decoder for one message level -> list of (field, wiretype, value),
+    raising WireError where the generated gogoproto Unmarshal fails: truncated data,
+    varints over 10 bytes, field number (key >> 3 as int32) <= 0, wire types 4, 6, 7.
+    A group (wire type 3) is skipped and listed with value None."""
     i, out = 0, []
     while i < len(buf):
         key, i = _read_varint(buf, i)
         field, wt = key >> 3, key & 7
+        f32 = field & 0xFFFFFFFF
+        if f32 == 0 or f32 >= 2**31:
+            raise WireError("illegal tag")
         if wt == 0:
             v, i = _read_varint(buf, i)
         elif wt == 2:
             ln, i = _read_varint(buf, i)
+            if ln > len(buf) - i:
+                raise WireError("unexpected EOF")
             v = buf[i:i + ln]
             i += ln
-        elif wt == 1:
-            v = buf[i:i + 8]
-            i += 8
-        elif wt == 5:
-            v = buf[i:i + 4]
-            i += 4
+        elif wt == 1 or wt == 5:
+            n = 8 if wt == 1 else 4
+            if len(buf) - i < n:
+                raise WireError("unexpected EOF")
+            v = buf[i:i + n]
+            i += n
+        elif wt == 3:
+            i = _skip_group(buf, i)
+            v = None
         else:
-            raise ValueError("bad wire type")
-        out.append((field, wt, v))
+            raise WireError("illegal wire type")
+        out.append((f32, wt, v))
     return out
 
 
 def unmarshal_blob_tx(tx: bytes):
-    """BlobTx {1: tx, 2: repeated Blob, 3: type_id "BLOB"} (proto/celestia/core/v1/blob/blob.proto)."""
-    if not tx.endswith(b"BLOB"):
-        return None
+    """go-square blob.UnmarshalBlobTx (the two-value form the reference calls,
+    pkg/proof/proof.go:52): BlobTx {1: tx, 2: repeated Blob, 3: type_id}
+    (proto/celestia/core/v1/blob/blob.proto). None (not a blob tx) unless the message
+    decodes, its type_id is "BLOB", it has blobs and every namespace id is 28 bytes.
+    A known field with another wire type is a decode error; repeated scalar fields keep
+    the last value; share_version / namespace_version are uint32 (varint truncated)."""
     try:
         fields = parse_proto(tx)
-    except (IndexError, ValueError):
+        inner, type_id, blobs = b"", b"", []
+        for f, wt, v in fields:
+            if f in (1, 2, 3) and wt != 2:
+                return None
+            if f == 1:
+                inner = bytes(v)
+            elif f == 3:
+                type_id = bytes(v)
+            elif f == 2:
+                b = {1: b"", 2: b"", 3: 0, 4: 0}
+                for bf, bwt, bv in parse_proto(v):
+                    if bf in (1, 2) and bwt != 2 or bf in (3, 4) and bwt != 0:
+                        return None
+                    if bf in (1, 2, 3, 4):
+                        b[bf] = bv if bf in (1, 2) else bv & 0xFFFFFFFF
+                blobs.append(b)
+    except WireError:
         return None
-    if not any(f == 3 and v == b"BLOB" for f, _, v in fields):
+    if type_id != b"BLOB" or not blobs or any(len(b[1]) != 28 for b in blobs):
         return None
-    inner = [v for f, _, v in fields if f == 1][0]
-    blobs = []
-    for f, _, v in fields:
-        if f != 2:
-            continue
-        b = {1: b"", 2: b"", 3: 0, 4: 0}
-        for bf, _, bv in parse_proto(v):
-            b[bf] = bv
-        blobs.append({"ns": bytes([b[4]]) + bytes(b[1]), "data": bytes(b[2]), "share_version": b[3]})
-    return inner, blobs
+    return inner, [{"ns": bytes([b[4] & 0xFF]) + bytes(b[1]), "data": bytes(b[2]), "share_version": b[3]}
+                   for b in blobs]
 
 
 def index_wrapper(tx: bytes, share_indexes) -> bytes:
@@ -151,7 +208,7 @@ def sparse_shares(blob) -> list:
     ns, data, ver = blob["ns"], blob["data"], blob["share_version"]
     shares, pos, first = [], 0, True
     while pos < len(data) or first:
-        head = ns + bytes([(ver << 1) | (1 if first else 0)])
+        head = ns + bytes([((ver << 1) | (1 if first else 0)) & 0xFF])  # the product truncates too
         if first:
             head += len(data).to_bytes(4, "big")
         cap = SHARE - len(head)
