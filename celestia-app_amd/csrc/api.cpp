@@ -795,6 +795,7 @@ struct RepairBufs {
 // synchronised: every flag is read back once at the end of the repair.
 static cel_status axes_pass(cel_ctx* ctx, const RepairBufs& b, uint32_t k, int is_col,
                             const std::vector<int32_t>& list, bool decode) {
+  const Range range(decode ? "repair.solve" : "repair.check");
   const uint32_t W = 2 * k, na = (uint32_t)list.size();
   if (!na) return CEL_OK;
   hipStream_t s = ctx->stream;

@@ -1,6 +1,7 @@
 // Internal declarations shared by the HIP kernels and the C-ABI host layer.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <cstddef>
 #include <cstdint>
@@ -49,6 +50,15 @@ struct DeviceTables {
   uint16_t* log16 = nullptr;   // [65536]
   uint16_t* skew16 = nullptr;  // [65535]
   uint32_t* mul8 = nullptr;    // [256][8] GF(2^8) product tables indexed by log value (decoder)
+};
+
+// roctx range over a phase's launches (rocprofv3 --marker-trace shows them on the host
+// timeline; the launches themselves are asynchronous, so a range brackets their enqueue).
+struct Range {
+  explicit Range(const char* name) { roctxRangePushA(name); }
+  ~Range() { roctxRangePop(); }
+  Range(const Range&) = delete;
+  Range& operator=(const Range&) = delete;
 };
 
 // XCD-aware workgroup order. Workgroups are dealt round-robin over the 8 XCDs

@@ -484,10 +484,13 @@ hipError_t launch_commit(const uint8_t* eds, uint32_t k, uint32_t nsq, uint8_t* 
   base += align256((size_t)nsq * 4 + 4);
   uint32_t* leafd = reinterpret_cast<uint32_t*>(base);
 
-  hipLaunchKernelGGL(k_fill_i32, dim3((nsq + 255) / 256), dim3(256), 0, s, bad, nsq, INT_MAX);
-  dim3 gl((W * W + 255) / 256, nsq);
-  if (order_check) hipLaunchKernelGGL(k_leaf<true>, gl, dim3(256), 0, s, eds, k, leaves, bad);
-  else hipLaunchKernelGGL(k_leaf<false>, gl, dim3(256), 0, s, eds, k, leaves, bad);
+  {
+    const Range r("nmt.leaf");
+    hipLaunchKernelGGL(k_fill_i32, dim3((nsq + 255) / 256), dim3(256), 0, s, bad, nsq, INT_MAX);
+    dim3 gl((W * W + 255) / 256, nsq);
+    if (order_check) hipLaunchKernelGGL(k_leaf<true>, gl, dim3(256), 0, s, eds, k, leaves, bad);
+    else hipLaunchKernelGGL(k_leaf<false>, gl, dim3(256), 0, s, eds, k, leaves, bad);
+  }
 
   // One launch per tree level, all 4k trees of all squares at once: every lane hashes
   // one node, no idle lanes. The last level writes the root records.
@@ -496,6 +499,7 @@ hipError_t launch_commit(const uint8_t* eds, uint32_t k, uint32_t nsq, uint8_t* 
   const uint32_t* src = leaves;
   uint32_t* dst = ping;
   bool first = true;
+  roctxRangePushA("nmt.levels");
   while (nin > 1) {
     const uint32_t nout = nin / 2;
     uint32_t* out = (nout == 1) ? roots : dst;
@@ -510,8 +514,10 @@ hipError_t launch_commit(const uint8_t* eds, uint32_t k, uint32_t nsq, uint8_t* 
     dst = (dst == ping) ? pong : ping;
     nin = nout;
   }
+  roctxRangePop();
   const size_t lds = (size_t)trees * 8 * 4;
   // roots already packed into row_roots / col_roots by the root level
+  const Range r("dah");
   if (dah)
     hipLaunchKernelGGL(k_merkle, dim3(nsq), dim3(256), lds, s, roots, leafd, trees, dah, nullptr, nullptr, bad, status);
   return hipGetLastError();

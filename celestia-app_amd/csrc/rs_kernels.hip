@@ -319,7 +319,10 @@ hipError_t launch_extend(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t 
   const uint64_t sq_eds = (uint64_t)4 * k * k * kShare;
   hipError_t e;
   // Q0 rows -> Q1 (reading the ODS and writing Q0 into the EDS on the way when ods != nullptr)
-  if ((e = launch_rs_encode(row_geom(ods, eds, k, nsq), t, s)) != hipSuccess) return e;
+  {
+    const Range r("rs.rows");
+    if ((e = launch_rs_encode(row_geom(ods, eds, k, nsq), t, s)) != hipSuccess) return e;
+  }
   // columns of [Q0|Q1] -> [Q2|Q3]
   RsGeom cols{};
   cols.in = eds;
@@ -334,6 +337,7 @@ hipError_t launch_extend(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t 
   cols.len = kShare;
   cols.axes = 2 * k;
   cols.nsq = nsq;
+  const Range r("rs.cols");
   return launch_rs_encode(cols, t, s);
 }
 
