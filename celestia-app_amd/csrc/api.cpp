@@ -99,10 +99,6 @@ cel_status cel_ctx_create(int device, cel_ctx** out) {
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_rs[i], hipEventDisableTiming);
   }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_start, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_sync, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventRecord(ctx->ev_sync, ctx->stream);
-  if (e == hipSuccess)
-    e = hipMalloc(reinterpret_cast<void**>(&ctx->sync), (size_t)(cel_ctx::kPipe + 1) * kSyncWords * 4);
   if (e == hipSuccess) e = upload_tables(&ctx->tables);
   if (e != hipSuccess) {
     cel_ctx_destroy(ctx);
@@ -127,8 +123,6 @@ void cel_ctx_destroy(cel_ctx* ctx) {
       if (ctx->ev_rs[i]) (void)hipEventDestroy(ctx->ev_rs[i]);
     }
     if (ctx->ev_start) (void)hipEventDestroy(ctx->ev_start);
-    if (ctx->ev_sync) (void)hipEventDestroy(ctx->ev_sync);
-    if (ctx->sync) (void)hipFree(ctx->sync);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   }
   delete ctx;
@@ -235,13 +229,8 @@ cel_status cel_dev_extend_only(cel_ctx* ctx, const void* d_ods, uint32_t n, uint
   cel_status st = validate_square(ctx, k, kShare);
   if (st) return st;
   DeviceGuard g(ctx->device);
-  // the extend_only slot: this launch after the previous one that used it, on any stream
-  hipStream_t us = pick_stream(ctx, stream);
-  hipError_t e = hipStreamWaitEvent(us, ctx->ev_sync, 0);
-  if (e == hipSuccess)
-    e = launch_extend(static_cast<const uint8_t*>(d_ods), static_cast<uint8_t*>(d_eds), k, n, ctx->tables, us,
-                      ctx->sync + (size_t)cel_ctx::kPipe * kSyncWords);
-  if (e == hipSuccess) e = hipEventRecord(ctx->ev_sync, us);
+  const hipError_t e = launch_extend(static_cast<const uint8_t*>(d_ods), static_cast<uint8_t*>(d_eds), k, n,
+                                     ctx->tables, pick_stream(ctx, stream));
   return e == hipSuccess ? CEL_OK : hip_fail(ctx, e, "extend");
 }
 
@@ -279,9 +268,7 @@ cel_status cel_dev_extend_batch(cel_ctx* ctx, const void* d_ods, uint32_t n, uin
     if ((e = hipStreamWaitEvent(s, ctx->ev_start, 0)) != hipSuccess) break;
     const uint8_t* ods = d_ods ? static_cast<const uint8_t*>(d_ods) + first * ods_sq : nullptr;
     uint8_t* eds = static_cast<uint8_t*>(d_eds) + first * eds_sq;
-    if ((e = launch_extend(ods, eds, k, cnt, ctx->tables, s, ctx->sync + (size_t)(c % cel_ctx::kPipe) * kSyncWords)) !=
-        hipSuccess)
-      break;
+    if ((e = launch_extend(ods, eds, k, cnt, ctx->tables, s)) != hipSuccess) break;
     if ((e = hipEventRecord(ctx->ev_rs[c], s)) != hipSuccess) break;
     e = launch_commit(eds, k, cnt, static_cast<uint8_t*>(d_row_roots) + first * roots_sq,
                       static_cast<uint8_t*>(d_col_roots) + first * roots_sq, static_cast<uint8_t*>(d_dah) + first * 32,
@@ -336,8 +323,7 @@ cel_status cel_extend_batch(cel_ctx* ctx, const uint8_t* ods, uint32_t n, uint32
     uint8_t* eds_c = d_eds + first * eds_sq;
     if ((e = hipStreamWaitEvent(cs, ctx->ev_start, 0)) != hipSuccess ||
         (e = place_ods(ods + first * ods_sq, cnt, k, eds_c, cs)) != hipSuccess ||
-        (e = launch_extend(nullptr, eds_c, k, cnt, ctx->tables, cs,
-                           ctx->sync + (size_t)(c % cel_ctx::kPipe) * kSyncWords)) != hipSuccess ||
+        (e = launch_extend(nullptr, eds_c, k, cnt, ctx->tables, cs)) != hipSuccess ||
         (e = launch_commit(eds_c, k, cnt, d_rr + first * roots_sq, d_cr + first * roots_sq, d_dah + first * 32,
                            d_st + first, d_work + (c % cel_ctx::kPipe) * ws, (flags & CEL_FLAG_ORDER_CHECK) != 0,
                            cs)) != hipSuccess)

@@ -80,18 +80,10 @@ hipError_t launch_rs_encode(const RsGeom& g, const DeviceTables& t, hipStream_t 
 hipError_t launch_rs_encode_bitslice(const RsGeom& g, hipStream_t s);  // GF(2^8), n <= 16
 hipError_t launch_rs_encode_axis(const RsGeom& g, hipStream_t s);       // GF(2^8), 32 <= n <= 128
 hipError_t launch_rs_encode_gf16x(const RsGeom& g, hipStream_t s);     // GF(2^16), n = 256 / 512
-// Both passes of the extension of nsq squares (32 <= k <= 128) in one launch with a
-// dequeue-ordered tile queue (rs_axis.hip). d_sync: kSyncWords words of a slot no other
-// launch uses concurrently. wait_q0: the row pass writes Q0 (separate ODS input).
-constexpr uint32_t kMaxFusedSquares = 4096;
-constexpr uint32_t kSyncWords = 2 + 2 * kMaxFusedSquares;
-hipError_t launch_extend_fused(const RsGeom& rows, const RsGeom& cols, uint32_t nsq, bool wait_q0, uint32_t* d_sync,
-                               hipStream_t s);
 // Full 2D extension of nsq squares: Q0 rows -> Q1, then all 2k columns -> Q2|Q3.
 // ods == nullptr means Q0 is already in place inside eds.
-// d_sync (nullable): a sync slot for the fused one-launch schedule (k = 32..128).
 hipError_t launch_extend(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t nsq,
-                         const DeviceTables& t, hipStream_t s, uint32_t* d_sync = nullptr);
+                         const DeviceTables& t, hipStream_t s);
 
 // NMT + DAH over resident EDSs. work: scratch of nmt_workspace_size(k, nsq) bytes.
 size_t nmt_workspace_size(uint32_t k, uint32_t nsq);
@@ -162,10 +154,6 @@ struct cel_ctx {
   hipStream_t stream = nullptr;
   hipStream_t sub[kPipe] = {nullptr, nullptr, nullptr, nullptr};
   hipEvent_t ev_start = nullptr;
-  // Sync slots of the fused extension: slot i < kPipe belongs to stream sub[i], slot kPipe
-  // to the cel_dev_extend_only calls (ordered among themselves by ev_sync).
-  uint32_t* sync = nullptr;  // [kPipe + 1][kSyncWords]
-  hipEvent_t ev_sync = nullptr;
   hipEvent_t ev_done[kChunks] = {};
   hipEvent_t ev_rs[kChunks] = {};
   std::mutex mu;

@@ -14,8 +14,6 @@
 // an 8/8/4-entry product table (as rs_kernels.hip gf8_mul4).
 #include <hip/hip_runtime.h>
 
-#include <algorithm>
-
 #include "cel_internal.hpp"
 #include "bitslice8.hpp"
 #include "gf8_constexpr.hpp"
@@ -221,11 +219,16 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
 }
 
-// Tile = (square z, axis x, 256-byte slice y) of geometry g: one wave. LP / SP: cache
-// policy of the loads / stores (2 = nt).
-template <int LOGK, int LP, int SP>
-__device__ __forceinline__ void axis_tile(const RsGeom& g, uint32_t nslice, uint32_t tile, uint32_t lane) {
+// Tile = (square z, axis x, 256-byte slice y): one wave. Loads and stores are nt
+// (non-temporal): every byte is touched once per pass and a batch is far larger than the
+// Infinity Cache (k=128, 256 squares: 9.35 -> 9.00 us per square against the default
+// policy, profiles/r1d_rs_cache_policy_ab.txt).
+template <int LOGK>
+__global__ __launch_bounds__(256, 3) void k_rs_axis_gf8(RsGeom g, uint32_t nslice) {
   constexpr int K = 1 << LOGK;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t tile = __builtin_amdgcn_readfirstlane(xcd_block(blockIdx.x, gridDim.x) * 4u + (threadIdx.x >> 6));
+  if (tile >= g.axes * nslice * g.nsq) return;
   const uint32_t y = tile % nslice, r = tile / nslice;
   const uint32_t x = r % g.axes, z = r / g.axes;
   const uint32_t col = y * 256u + lane * 4u;
@@ -236,12 +239,12 @@ __device__ __forceinline__ void axis_tile(const RsGeom& g, uint32_t nslice, uint
     const auto rin = rsrc(g.in + (uint64_t)z * g.in_sq + (uint64_t)x * g.in_axis + (uint64_t)y * 256u);
     const uint32_t in_shard = (uint32_t)g.in_shard;
 #pragma unroll
-    for (int i = 0; i < K; i++) w[i] = __builtin_amdgcn_raw_buffer_load_b32(rin, lo, (uint32_t)i * in_shard, LP);
+    for (int i = 0; i < K; i++) w[i] = __builtin_amdgcn_raw_buffer_load_b32(rin, lo, (uint32_t)i * in_shard, 2);
     if (g.dcopy && active) {
       const auto rdc = rsrc(g.dcopy + (uint64_t)z * g.dc_sq + (uint64_t)x * g.dc_axis + (uint64_t)y * 256u);
       const uint32_t dc_shard = (uint32_t)g.dc_shard;
 #pragma unroll
-      for (int i = 0; i < K; i++) __builtin_amdgcn_raw_buffer_store_b32(w[i], rdc, lo, (uint32_t)i * dc_shard, SP);
+      for (int i = 0; i < K; i++) __builtin_amdgcn_raw_buffer_store_b32(w[i], rdc, lo, (uint32_t)i * dc_shard, 2);
     }
   }
   transform_hyb<K>(w);
@@ -249,128 +252,7 @@ __device__ __forceinline__ void axis_tile(const RsGeom& g, uint32_t nslice, uint
     const auto rout = rsrc(g.out + (uint64_t)z * g.out_sq + (uint64_t)x * g.out_axis + (uint64_t)y * 256u);
     const uint32_t out_shard = (uint32_t)g.out_shard;
 #pragma unroll
-    for (int i = 0; i < K; i++) __builtin_amdgcn_raw_buffer_store_b32(w[i], rout, lo, (uint32_t)i * out_shard, SP);
-  }
-}
-
-// One pass (rows or columns) of every square of g. Loads and stores are nt (non-temporal):
-// every byte is touched once per pass and a batch is far larger than the Infinity Cache
-// (k=128, 256 squares: 9.35 -> 9.00 us per square against the default policy,
-// profiles/r1d_rs_cache_policy_ab.txt).
-template <int LOGK>
-__global__ __launch_bounds__(256, 3) void k_rs_axis_gf8(RsGeom g, uint32_t nslice) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t tile = __builtin_amdgcn_readfirstlane(xcd_block(blockIdx.x, gridDim.x) * 4u + (threadIdx.x >> 6));
-  if (tile >= g.axes * nslice * g.nsq) return;
-  axis_tile<LOGK, 2, 2>(g, nslice, tile, lane);
-}
-
-// Both passes of the extension in one launch, as a dequeue-ordered tile queue.
-//
-// Every wave takes tickets from one atomic counter and runs the tile its ticket names
-// until the tickets run out. Ticket order: for block j = 0, 1, ..: the row tiles of
-// square j, then its Q0 column tiles, then the Q1 column tiles of square j - kLag. A Q1
-// column tile (column x >= k, slice y) needs the outputs of all k row tiles of slice y of
-// its square; those carry smaller tickets, so they were dequeued by waves that are
-// already running and that wait on nothing. That is the forward-progress argument a
-// blockIdx-ordered version lacks: there a waiting tile may hold the
-// CU slot that the tile it waits on needs, because dispatch order does not guarantee
-// residency. Hand-off (cdna_hip_programming.md Guideline 16, write-through form R1): the
-// row tile stores its output sc1 (write-through, so no release fence: a buffer_wbl2 per
-// tile flushes the whole XCD L2 and made a first version 4x slower), waits for its
-// stores (s_waitcnt vmcnt(0)), then adds 1 to the (square, slice) counter at agent scope;
-// the consumer polls with agent-scope atomics (wait_count) and reads every handed-off
-// byte with sc1 loads, which need no acquire. A poll loop that exceeds its budget (only possible with a bug) gives up and
-// raises sync[1], so every wave reaches the exit.
-//
-// Cache policy: the row tiles load with the default policy (their Q0 rows are read again
-// by the Q0 column tiles a few hundred tickets later), the column tiles store nt.
-struct FusedExt {
-  RsGeom rows, cols;  // row pass (Q0 rows -> Q1) and column pass (all 2k columns)
-  uint32_t* sync;     // [0] ticket, [1] poll budget exceeded, [2 + 2s + y] row tiles done
-  uint32_t nsq;
-  uint32_t wait_q0;   // the row pass writes Q0 (separate ODS input): Q0 column tiles wait too
-};
-constexpr uint32_t kLag = 4;  // squares between a square's row tiles and its Q1 column tiles
-constexpr int kSc1 = 16;      // buffer aux bit of sc1
-
-// ticket -> (square, kind, index inside the kind's 2K tiles); kind 0 rows, 1 Q0 cols, 2 Q1 cols
-__device__ __forceinline__ void fused_ticket(uint32_t t, uint32_t K, uint32_t nsq, uint32_t& sq, uint32_t& kind,
-                                             uint32_t& u) {
-  const uint32_t lag = nsq < kLag ? nsq : kLag;
-  const uint32_t head = lag * 4 * K;                  // blocks 0 .. lag-1: rows + Q0 cols
-  const uint32_t body = (nsq - lag) * 6 * K;          // blocks lag .. nsq-1: + Q1 cols of j - lag
-  uint32_t j, v;
-  if (t < head) {
-    j = t / (4 * K);
-    v = t % (4 * K);
-  } else if (t < head + body) {
-    j = lag + (t - head) / (6 * K);
-    v = (t - head) % (6 * K);
-  } else {  // tail: Q1 cols of the last `lag` squares
-    const uint32_t r = t - head - body;
-    sq = nsq - lag + r / (2 * K);
-    kind = 2;
-    u = r % (2 * K);
-    return;
-  }
-  if (v < 4 * K) {
-    sq = j;
-    kind = v / (2 * K);
-    u = v % (2 * K);
-  } else {
-    sq = j - lag;
-    kind = 2;
-    u = v - 4 * K;
-  }
-}
-
-// One lane takes the wave's ticket; every lane gets it.
-__device__ __forceinline__ uint32_t next_ticket(uint32_t* ctr, uint32_t lane) {
-  uint32_t v = 0;
-  if (lane == 0) v = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return __builtin_amdgcn_readfirstlane(v);
-}
-
-// Waits until *ctr reaches `target`: one lane polls with relaxed agent-scope loads (sc1,
-// L1 bypassed), sleeping ~1 us between polls. (Polling with atomic read-modify-writes
-// queued the polls with the producers' adds on the same word and ran 4x slower.) false
-// after the poll budget (sync[1] raised by the caller).
-__device__ __forceinline__ bool wait_count(uint32_t* ctr, uint32_t target, uint32_t lane) {
-  for (uint32_t polls = 0; polls < (1u << 16); polls++) {
-    uint32_t v = 0;
-    if (lane == 0) v = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (__builtin_amdgcn_readfirstlane(v) >= target) return true;
-    __builtin_amdgcn_s_sleep(32);
-  }
-  return false;
-}
-
-template <int LOGK>
-__global__ __launch_bounds__(256, 3) void k_rs_extend_fused(FusedExt f) {
-  constexpr uint32_t K = 1u << LOGK;
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t total = 6 * K * f.nsq;
-  for (uint32_t t = next_ticket(f.sync, lane); t < total; t = next_ticket(f.sync, lane)) {
-    uint32_t sq, kind, u;
-    fused_ticket(t, K, f.nsq, sq, kind, u);
-    const uint32_t y = u / K, x = u % K;  // slice-major: slice 0's tiles first
-    uint32_t* cnt = f.sync + 2 + 2 * sq + y;
-    if (kind == 0) {
-      axis_tile<LOGK, 0, kSc1>(f.rows, 2, (sq * K + x) * 2 + y, lane);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every sc1 store of this wave is out
-      if (lane == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      const uint32_t tile = (sq * 2 * K + (kind == 2 ? K : 0) + x) * 2 + y;
-      if (kind == 2 || f.wait_q0) {
-        if (!wait_count(cnt, K, lane) && lane == 0)
-          __hip_atomic_store(f.sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the loads below the poll
-        axis_tile<LOGK, kSc1, 2>(f.cols, 2, tile, lane);
-      } else {
-        axis_tile<LOGK, 2, 2>(f.cols, 2, tile, lane);
-      }
-    }
+    for (int i = 0; i < K; i++) __builtin_amdgcn_raw_buffer_store_b32(w[i], rout, lo, (uint32_t)i * out_shard, 2);
   }
 }
 
@@ -390,38 +272,6 @@ hipError_t launch(const RsGeom& g, hipStream_t s) {
 static bool geom_ok(const RsGeom& g) {
   const uint64_t span = (uint64_t)g.n * (g.in_shard > g.out_shard ? g.in_shard : g.out_shard) + g.len;
   return span < 0x7fffffffull && !(g.dcopy && (uint64_t)g.n * g.dc_shard + g.len >= 0x7fffffffull);
-}
-
-// Waves of the fused launch: three 4-wave workgroups per CU (168 VGPRs).
-static uint32_t fused_workgroups() {
-  static const uint32_t v = [] {
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                               hipSuccess || cus <= 0)
-      cus = 256;
-    return (uint32_t)cus * 3u;
-  }();
-  return v;
-}
-
-hipError_t launch_extend_fused(const RsGeom& rows, const RsGeom& cols, uint32_t nsq, bool wait_q0, uint32_t* d_sync,
-                               hipStream_t s) {
-  const uint32_t k = rows.n;
-  if (nsq == 0) return hipSuccess;
-  if (!d_sync || nsq > kMaxFusedSquares || rows.len != 512 || cols.len != 512 || !geom_ok(rows) || !geom_ok(cols))
-    return hipErrorInvalidValue;
-  hipError_t e = hipMemsetAsync(d_sync, 0, (2 + 2 * (size_t)nsq) * 4, s);
-  if (e != hipSuccess) return e;
-  ax::FusedExt f{rows, cols, d_sync, nsq, wait_q0 ? 1u : 0u};
-  const uint64_t waves = (uint64_t)6 * k * nsq;
-  const uint32_t wgs = (uint32_t)std::min<uint64_t>((waves + 3) / 4, fused_workgroups());
-  switch (k) {
-    case 32: hipLaunchKernelGGL(ax::k_rs_extend_fused<5>, dim3(wgs), dim3(256), 0, s, f); break;
-    case 64: hipLaunchKernelGGL(ax::k_rs_extend_fused<6>, dim3(wgs), dim3(256), 0, s, f); break;
-    case 128: hipLaunchKernelGGL(ax::k_rs_extend_fused<7>, dim3(wgs), dim3(256), 0, s, f); break;
-    default: return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
 }
 
 hipError_t launch_rs_encode_axis(const RsGeom& g, hipStream_t s) {

@@ -313,11 +313,16 @@ static RsGeom row_geom(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t ns
 }
 
 hipError_t launch_extend(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t nsq, const DeviceTables& t,
-                         hipStream_t s, uint32_t* d_sync) {
+                         hipStream_t s) {
   if (nsq == 0) return hipSuccess;
   const uint64_t row = (uint64_t)2 * k * kShare;  // bytes per EDS row
   const uint64_t sq_eds = (uint64_t)4 * k * k * kShare;
-  const RsGeom rows = row_geom(ods, eds, k, nsq);
+  hipError_t e;
+  // Q0 rows -> Q1 (reading the ODS and writing Q0 into the EDS on the way when ods != nullptr)
+  {
+    const Range r("rs.rows");
+    if ((e = launch_rs_encode(row_geom(ods, eds, k, nsq), t, s)) != hipSuccess) return e;
+  }
   // columns of [Q0|Q1] -> [Q2|Q3]
   RsGeom cols{};
   cols.in = eds;
@@ -332,15 +337,6 @@ hipError_t launch_extend(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t 
   cols.len = kShare;
   cols.axes = 2 * k;
   cols.nsq = nsq;
-  if (d_sync && k >= 32 && k <= 128 && nsq <= kMaxFusedSquares) {
-    const Range r("rs.fused");
-    return launch_extend_fused(rows, cols, nsq, ods != nullptr, d_sync, s);
-  }
-  hipError_t e;
-  {  // Q0 rows -> Q1 (reading the ODS and writing Q0 into the EDS on the way when ods != nullptr)
-    const Range r("rs.rows");
-    if ((e = launch_rs_encode(rows, t, s)) != hipSuccess) return e;
-  }
   const Range r("rs.cols");
   return launch_rs_encode(cols, t, s);
 }
