@@ -76,16 +76,27 @@ class DataAvailabilityHeader:
         self.hash = b""
 
     def Hash(self):
+        """data_availability_header.go:92-108: merkle.HashFromByteSlices over the
+        rowsCount row roots followed by the first rowsCount column roots (nil slices where
+        there are fewer columns), roots of any length. 90-byte roots with as many columns
+        as rows take the NMT-root kernel (cel_dah_hash), anything else the generic one
+        (cel_merkle_hash_slices)."""
         if self.hash:
             return self.hash
         ctx = _lib.default_context()
         w = len(self.RowRoots)
         out = np.zeros(32, np.uint8)
-        if w != len(self.ColumnRoots) or any(len(r) != _lib.NMT_NODE_SIZE for r in self.RowRoots + self.ColumnRoots):
-            raise CelError(_lib.EINVAL, "DAH roots must be 90-byte NMT roots with as many rows as columns")
-        rr = np.frombuffer(b"".join(self.RowRoots), np.uint8).copy() if w else np.zeros(1, np.uint8)
-        cr = np.frombuffer(b"".join(self.ColumnRoots), np.uint8).copy() if w else np.zeros(1, np.uint8)
-        ctx.check(ctx.lib.cel_dah_hash(ctx.handle, _p(rr), _p(cr), w, _p(out)))
+        if w == len(self.ColumnRoots) and all(len(r) == _lib.NMT_NODE_SIZE for r in self.RowRoots + self.ColumnRoots):
+            rr = np.frombuffer(b"".join(self.RowRoots), np.uint8).copy() if w else np.zeros(1, np.uint8)
+            cr = np.frombuffer(b"".join(self.ColumnRoots), np.uint8).copy() if w else np.zeros(1, np.uint8)
+            ctx.check(ctx.lib.cel_dah_hash(ctx.handle, _p(rr), _p(cr), w, _p(out)))
+        else:
+            cols = list(self.ColumnRoots[:w]) + [b""] * max(0, w - len(self.ColumnRoots))
+            slices = [bytes(r) for r in self.RowRoots] + [bytes(c) for c in cols]
+            offs = np.zeros(len(slices) + 1, np.uint64)
+            offs[1:] = np.cumsum([len(x) for x in slices], dtype=np.uint64) if slices else []
+            data = np.frombuffer(b"".join(slices) or b"\0", np.uint8).copy()
+            ctx.check(ctx.lib.cel_merkle_hash_slices(ctx.handle, _p(data), _p(offs), len(slices), _p(out)))
         self.hash = out.tobytes()
         return self.hash
 

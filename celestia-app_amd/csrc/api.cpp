@@ -642,6 +642,35 @@ cel_status cel_dah_hash(cel_ctx* ctx, const uint8_t* row_roots, const uint8_t* c
   return CEL_OK;
 }
 
+cel_status cel_merkle_hash_slices(cel_ctx* ctx, const uint8_t* data, const uint64_t* offsets, uint32_t n,
+                                  uint8_t* out) {
+  if (!ctx) return CEL_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (!out || !offsets || (n && !data && offsets[n] > offsets[0])) return fail(ctx, CEL_EINVAL, "nil argument");
+  for (uint32_t i = 0; i < n; i++)
+    if (offsets[i + 1] < offsets[i]) return fail(ctx, CEL_EINVAL, "slice offsets must be non-decreasing");
+  if (n > (1u << 20)) return fail(ctx, CEL_ETOOBIG, "too many slices for the device merkle kernel");
+  const uint64_t bytes = n ? offsets[n] - offsets[0] : 0;
+  DeviceGuard g(ctx->device);
+  hipError_t e = hipSuccess;
+  const size_t ob = ((size_t)(n + 1) * 8 + 255) / 256 * 256;
+  uint8_t* d_in = static_cast<uint8_t*>(scratch(ctx, S_IN, ob + (bytes ? bytes : 1), &e));
+  void* d_w = scratch(ctx, S_WORK, slices_workspace_size(n), &e);
+  uint8_t* d_o = static_cast<uint8_t*>(scratch(ctx, S_ROOTS, 256, &e));
+  if (!d_in || !d_w || !d_o) return fail(ctx, CEL_ENOMEM, "device allocation failed");
+  std::vector<uint64_t> off(n + 1);
+  for (uint32_t i = 0; i <= n; i++) off[i] = offsets[i] - offsets[0];
+  hipStream_t s = ctx->stream;
+  if ((e = hipMemcpyAsync(d_in, off.data(), (size_t)(n + 1) * 8, hipMemcpyHostToDevice, s)) != hipSuccess ||
+      (bytes && (e = hipMemcpyAsync(d_in + ob, data + offsets[0], bytes, hipMemcpyHostToDevice, s)) != hipSuccess))
+    return hip_fail(ctx, e, "H2D");
+  if ((e = launch_hash_slices(d_in + ob, reinterpret_cast<const uint64_t*>(d_in), n, d_o, d_w, s)) != hipSuccess)
+    return hip_fail(ctx, e, "merkle");
+  if ((e = hipMemcpyAsync(out, d_o, 32, hipMemcpyDeviceToHost, s)) != hipSuccess) return hip_fail(ctx, e, "D2H");
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "sync");
+  return CEL_OK;
+}
+
 // ------------------------------------------------------------- exported trees
 //
 // Inner nodes for proofs: pkg/proof/proof.go:151-201 rebuilds

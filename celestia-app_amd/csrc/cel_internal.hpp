@@ -101,6 +101,11 @@ size_t nmt_root_workspace_size(uint32_t n);
 hipError_t launch_merkle_root(const uint8_t* items, uint32_t n, uint32_t item_len, uint8_t* out,
                               void* work, hipStream_t s);
 size_t merkle_workspace_size(uint32_t n);
+// merkle.HashFromByteSlices over n slices of any length (data + off[i] .. off[i + 1]),
+// all device pointers; work: slices_workspace_size(n) bytes.
+hipError_t launch_hash_slices(const uint8_t* data, const uint64_t* off, uint32_t n, uint8_t* out, void* work,
+                              hipStream_t s);
+size_t slices_workspace_size(uint32_t n);
 
 // Row-sharded mode (one column slab of one square per rank).
 size_t slab_workspace_size(uint32_t k, uint32_t w);

@@ -984,4 +984,61 @@ hipError_t launch_gather_nodes(const uint32_t* nodes, const int32_t* rec, uint32
   return hipGetLastError();
 }
 
+// merkle.HashFromByteSlices (tendermint crypto/merkle, RFC-6962) over n byte slices of any
+// length: the DAH hash when the roots are not all 90-byte NMT roots
+// (data_availability_header.go:92-108 hashes whatever RowRoots / ColumnRoots hold). Leaf
+// i = SHA256(0x00 || slice i), one lane each; then one workgroup pairs adjacent nodes
+// level by level, carrying an odd last node up unchanged, which is the same tree as the
+// reference's split at the largest power of two below n. n == 0: SHA256("").
+__global__ void k_slice_leaves(const uint8_t* __restrict__ data, const uint64_t* __restrict__ off, uint32_t n,
+                               uint32_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t st[8];
+  sha_bytes(data + off[i], (uint32_t)(off[i + 1] - off[i]), nullptr, 0, 0x00, st);
+  for (int j = 0; j < 8; j++) out[(uint64_t)i * 8 + j] = st[j];
+}
+
+__global__ __launch_bounds__(256) void k_slice_tree(uint32_t* __restrict__ a, uint32_t* __restrict__ b, uint32_t n,
+                                                    uint8_t* __restrict__ out) {
+  if (n == 0) {
+    if (threadIdx.x == 0) {
+      uint32_t st[8], w[16];
+      sha256_init(st);
+      w[0] = 0x80000000u;
+      for (int j = 1; j < 16; j++) w[j] = 0;
+      sha256_compress(st, w);
+      for (int j = 0; j < 32; j++) out[j] = (uint8_t)(st[j / 4] >> (24 - 8 * (j % 4)));
+    }
+    return;
+  }
+  uint32_t* src = a;
+  uint32_t* dst = b;
+  for (uint32_t m = n; m > 1; m = (m + 1) / 2) {  // ping-pong: a level reads src, writes dst
+    for (uint32_t i = threadIdx.x; i < m / 2; i += blockDim.x) {
+      uint32_t st[8];
+      rfc_inner(src + (uint64_t)(2 * i) * 8, src + (uint64_t)(2 * i + 1) * 8, st);
+      for (int j = 0; j < 8; j++) dst[(uint64_t)i * 8 + j] = st[j];
+    }
+    if ((m & 1) && threadIdx.x == 0)
+      for (int j = 0; j < 8; j++) dst[(uint64_t)(m / 2) * 8 + j] = src[(uint64_t)(m - 1) * 8 + j];
+    __syncthreads();
+    uint32_t* t = src;
+    src = dst;
+    dst = t;
+  }
+  if (threadIdx.x < 32) out[threadIdx.x] = (uint8_t)(src[threadIdx.x / 4] >> (24 - 8 * (threadIdx.x % 4)));
+}
+
+size_t slices_workspace_size(uint32_t n) { return 2 * align256((size_t)(n ? n : 1) * 32); }
+
+hipError_t launch_hash_slices(const uint8_t* data, const uint64_t* off, uint32_t n, uint8_t* out, void* work,
+                              hipStream_t s) {
+  uint32_t* a = static_cast<uint32_t*>(work);
+  uint32_t* b = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(work) + align256((size_t)(n ? n : 1) * 32));
+  if (n) hipLaunchKernelGGL(k_slice_leaves, dim3((n + 255) / 256), dim3(256), 0, s, data, off, n, a);
+  hipLaunchKernelGGL(k_slice_tree, dim3(1), dim3(256), 0, s, a, b, n, out);
+  return hipGetLastError();
+}
+
 }  // namespace cel

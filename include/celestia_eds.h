@@ -189,6 +189,14 @@ cel_status cel_nmt_root(cel_ctx* ctx, const uint8_t* leaves, uint32_t n, uint32_
 /* DataAvailabilityHeader.Hash: RFC-6962 root over rowRoots || colRoots (w each). */
 cel_status cel_dah_hash(cel_ctx* ctx, const uint8_t* row_roots, const uint8_t* col_roots,
                         uint32_t w, uint8_t* out);
+/* merkle.HashFromByteSlices (RFC-6962; tendermint crypto/merkle, the hash
+ * DataAvailabilityHeader.Hash applies to rowRoots || colRoots,
+ * data_availability_header.go:92-108) over n byte slices of any length: slice i is
+ * data[offsets[i] .. offsets[i+1]) (offsets: n + 1 entries, non-decreasing). For DAHs
+ * whose roots are not all 90-byte NMT roots (FromProto accepts any length). n = 0 gives
+ * SHA-256 of the empty string. */
+cel_status cel_merkle_hash_slices(cel_ctx* ctx, const uint8_t* data, const uint64_t* offsets, uint32_t n,
+                                  uint8_t* out);
 
 /* ------------------------------------------------------------------ repair
  * rsmt2d ExtendedDataSquare.Repair(rowRoots, colRoots) (rsmt2d v0.14.0

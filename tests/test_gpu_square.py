@@ -254,3 +254,37 @@ def test_parity_namespace_in_ods(ctx, oracle, k, region):
     assert np.array_equal(dev._row_roots, rr), "row roots differ"
     assert np.array_equal(dev._col_roots, cr), "column roots differ"
     assert dev._dah == dah
+
+
+def test_dah_hash_any_root_length(ctx):
+    """DataAvailabilityHeader.Hash over roots of any length and unequal row / column
+    counts (data_availability_header.go:92-108: rowsCount row roots, then the first
+    rowsCount column roots, nil slices where there are fewer) against a hashlib
+    merkle.HashFromByteSlices; 90-byte roots keep going through cel_dah_hash."""
+    import hashlib
+    from celestia_eds import da
+
+    def sha(b):
+        return hashlib.sha256(b).digest()
+
+    def rfc(items):
+        if not items:
+            return sha(b"")
+        if len(items) == 1:
+            return sha(b"\x00" + items[0])
+        k = 1
+        while k * 2 < len(items):
+            k *= 2
+        return sha(b"\x01" + rfc(items[:k]) + rfc(items[k:]))
+
+    rng = np.random.default_rng(7)
+    cases = [([], []), ([b"a"], [b"b"]), ([b"x" * 32] * 3, [b"y" * 32] * 3), ([b""] * 2, [b"z"] * 2),
+             ([bytes(rng.integers(0, 256, int(n), np.uint8)) for n in rng.integers(0, 300, 7)],
+              [bytes(rng.integers(0, 256, int(n), np.uint8)) for n in rng.integers(0, 300, 5)]),
+             ([b"r" * 90] * 4, [b"c" * 90] * 6),
+             ([bytes(rng.integers(0, 256, 90, np.uint8)) for _ in range(8)],
+              [bytes(rng.integers(0, 256, 90, np.uint8)) for _ in range(8)])]
+    for rows, cols in cases:
+        w = len(rows)
+        want = rfc(rows + (cols[:w] + [b""] * max(0, w - len(cols))))
+        assert da.DataAvailabilityHeader(rows, cols).Hash() == want, (len(rows), len(cols))
