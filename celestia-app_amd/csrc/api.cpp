@@ -115,6 +115,7 @@ void cel_ctx_destroy(cel_ctx* ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (int i = 0; i < 6; i++)
       if (ctx->scratch[i]) (void)hipFree(ctx->scratch[i]);
+    if (ctx->hstage) (void)hipHostFree(ctx->hstage);
     free_tables(&ctx->tables);
     for (int i = 0; i < cel_ctx::kPipe; i++)
       if (ctx->sub[i]) (void)hipStreamDestroy(ctx->sub[i]);
@@ -806,13 +807,22 @@ cel_status cel_get_commitment(cel_ctx* ctx, const uint8_t* eds, uint32_t k, uint
 // computation run on the device over the EDS kept resident.
 namespace {
 
+// Axis lists of the passes of one repair: each pass gets its own slot of a page-locked
+// host buffer and of the device index buffer, so its upload is asynchronous and no pass
+// waits for the previous one's kernels (a pageable upload into one shared buffer
+// serialised the host against the stream). Slots wrap with one stream sync.
+constexpr uint32_t kIdxSlots = 64;
+
 struct RepairBufs {
   uint8_t* eds;
   uint8_t* mask;
   uint8_t* dense;
   uint8_t* dmask;
   uint8_t* tmp;
-  int32_t* idx;
+  int32_t* idx;    // [kIdxSlots][W] device axis lists
+  int32_t* hidx;   // [kIdxSlots][W] page-locked staging of the same
+  uint8_t* hmask;  // [W][W] page-locked staging of the presence mask
+  uint32_t slot;   // next free slot
   int32_t* flags;  // [2][W] encoding-check flags by (direction, axis): an axis completes once
 };
 
@@ -822,16 +832,23 @@ struct RepairBufs {
 // decoded cells are scattered back into the square; otherwise they are complete already
 // (preRepairSanityCheck, and the orthogonal axes a solve completes). Nothing is
 // synchronised: every flag is read back once at the end of the repair.
-static cel_status axes_pass(cel_ctx* ctx, const RepairBufs& b, uint32_t k, int is_col,
-                            const std::vector<int32_t>& list, bool decode) {
+static cel_status axes_pass(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_col, const std::vector<int32_t>& list,
+                            bool decode) {
   const Range range(decode ? "repair.solve" : "repair.check");
   const uint32_t W = 2 * k, na = (uint32_t)list.size();
   if (!na) return CEL_OK;
   hipStream_t s = ctx->stream;
   hipError_t e;
-  if ((e = hipMemcpyAsync(b.idx, list.data(), na * 4, hipMemcpyHostToDevice, s)) != hipSuccess)
-    return hip_fail(ctx, e, "H2D");
-  if ((e = launch_gather_axes(b.eds, b.mask, W, b.idx, is_col, na, b.dense, b.dmask, s)) != hipSuccess)
+  if (b.slot == kIdxSlots) {  // every slot in flight: let them drain, then reuse
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "sync");
+    b.slot = 0;
+  }
+  int32_t* hidx = b.hidx + (size_t)b.slot * W;
+  int32_t* idx = b.idx + (size_t)b.slot * W;
+  b.slot++;
+  std::memcpy(hidx, list.data(), (size_t)na * 4);
+  if ((e = hipMemcpyAsync(idx, hidx, na * 4, hipMemcpyHostToDevice, s)) != hipSuccess) return hip_fail(ctx, e, "H2D");
+  if ((e = launch_gather_axes(b.eds, b.mask, W, idx, is_col, na, b.dense, b.dmask, s)) != hipSuccess)
     return hip_fail(ctx, e, "gather");
   if (decode && (e = launch_rs_decode(b.dense, b.dmask, na, k, kShare, ctx->tables, nullptr, s)) != hipSuccess)
     return hip_fail(ctx, e, "decode");
@@ -850,12 +867,10 @@ static cel_status axes_pass(cel_ctx* ctx, const RepairBufs& b, uint32_t k, int i
   g.nsq = 1;
   if ((e = launch_rs_encode(g, ctx->tables, s)) != hipSuccess) return hip_fail(ctx, e, "re-encode");
   if ((e = launch_cmp(b.tmp, (uint64_t)k * kShare, b.dense + (uint64_t)k * kShare, (uint64_t)W * kShare,
-                      (uint64_t)k * kShare, na, b.flags + (size_t)is_col * W, s, b.idx)) != hipSuccess)
+                      (uint64_t)k * kShare, na, b.flags + (size_t)is_col * W, s, idx)) != hipSuccess)
     return hip_fail(ctx, e, "compare");
-  if (decode && (e = launch_scatter_axes(b.eds, b.mask, W, b.idx, is_col, na, b.dense, s)) != hipSuccess)
+  if (decode && (e = launch_scatter_axes(b.eds, b.mask, W, idx, is_col, na, b.dense, s)) != hipSuccess)
     return hip_fail(ctx, e, "scatter");
-  // the next pass rewrites b.idx after these kernels (stream order); `list` stays alive
-  // in the caller until the final synchronisation
   return CEL_OK;
 }
 
@@ -872,7 +887,7 @@ struct Check {
 struct Solve {
   int is_col;
   int32_t idx;
-  std::vector<uint8_t> before;  // the axis's presence mask before the solve
+  size_t before;  // offset of the axis's presence mask before the solve (W bytes) in the log
 };
 
 struct RepairOut {
@@ -894,7 +909,8 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
   hipStream_t s = ctx->stream;
   hipError_t e = hipSuccess;
   cel_status st;
-  if ((e = hipMemcpyAsync(b.mask, hm.data(), cells, hipMemcpyHostToDevice, s)) != hipSuccess ||
+  std::memcpy(b.hmask, hm.data(), cells);
+  if ((e = hipMemcpyAsync(b.mask, b.hmask, cells, hipMemcpyHostToDevice, s)) != hipSuccess ||
       (e = hipMemsetAsync(b.flags, 0, 2 * (size_t)W * 4, s)) != hipSuccess)
     return hip_fail(ctx, e, "H2D");
   const std::vector<uint8_t> initial = hm;
@@ -902,15 +918,19 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
     return is_col ? hm[(size_t)j * W + i] : hm[(size_t)i * W + j];
   };
   std::vector<uint32_t> cnt[2] = {std::vector<uint32_t>(W, 0), std::vector<uint32_t>(W, 0)};  // known cells per axis
-  for (uint32_t i = 0; i < W; i++)
-    for (uint32_t j = 0; j < W; j++)
-      if (hm[(size_t)i * W + j]) {
-        cnt[0][i]++;
-        cnt[1][j]++;
-      }
+  for (uint32_t i = 0; i < W; i++) {  // hm holds 0/1: plain sums (vectorised)
+    const uint8_t* row = hm.data() + (size_t)i * W;
+    uint32_t c = 0;
+    for (uint32_t j = 0; j < W; j++) {
+      c += row[j];
+      cnt[1][j] += row[j];
+    }
+    cnt[0][i] = c;
+  }
   auto count = [&](int is_col, uint32_t i) { return cnt[is_col][i]; };
   std::vector<Check> order;
   std::vector<Solve> solves;
+  std::vector<uint8_t> befores;  // presence masks of the solved axes before their solves
   std::vector<std::vector<int32_t>> lists;  // kept alive until the final sync
   // preRepairSanityCheck: for i: row i, column i
   {
@@ -940,13 +960,19 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
       if ((st = axes_pass(ctx, b, k, is_col, list, true)) != CEL_OK) return st;
       // sequential view of the pass: solve i fills its missing cells, completing the
       // orthogonal axes whose only missing cell it was
+      befores.reserve(befores.size() + list.size() * W);
       for (int32_t i : list) {
-        Solve sv{is_col, i, std::vector<uint8_t>(W)};
-        for (uint32_t j = 0; j < W; j++) sv.before[j] = at(is_col, (uint32_t)i, j);
+        const Solve sv{is_col, i, befores.size()};
+        befores.resize(befores.size() + W);
+        uint8_t* bf = befores.data() + sv.before;
+        if (is_col)
+          for (uint32_t j = 0; j < W; j++) bf[j] = hm[(size_t)j * W + (uint32_t)i];
+        else
+          std::memcpy(bf, hm.data() + (size_t)i * W, W);
         const int32_t si = (int32_t)solves.size();
         order.push_back({Check::SOLVE, is_col, i, si});
         for (uint32_t j = 0; j < W; j++) {
-          if (sv.before[j]) continue;
+          if (bf[j]) continue;
           at(is_col, (uint32_t)i, j) = 1;
           cnt[is_col][i]++;
           if (++cnt[!is_col][j] == W) {
@@ -954,7 +980,7 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
             orth.push_back((int32_t)j);
           }
         }
-        solves.push_back(std::move(sv));
+        solves.push_back(sv);
       }
       std::sort(orth.begin(), orth.end());
       if ((st = axes_pass(ctx, b, k, !is_col, orth, false)) != CEL_OK) return st;
@@ -1034,7 +1060,7 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
       case Check::SOLVE:
         if (!enc_ok(c.is_col, c.idx) || !root_ok(c.is_col, c.idx)) {
           rollback(c.solve);
-          return fail_axis(CEL_EBYZANTINE, c.is_col, c.idx, solves[c.solve].before.data());
+          return fail_axis(CEL_EBYZANTINE, c.is_col, c.idx, befores.data() + solves[c.solve].before);
         }
         break;
       case Check::ORTH:
@@ -1057,14 +1083,26 @@ static cel_status repair_bufs(cel_ctx* ctx, uint32_t k, bool own_eds, RepairBufs
   // dense doubles as the commit workspace of the final verification
   const size_t dense_b = std::max(eds_b, nmt_workspace_size(k, 1));
   b->dense = static_cast<uint8_t*>(scratch(ctx, S_IN, dense_b, &e));
-  b->tmp = static_cast<uint8_t*>(scratch(ctx, S_AUX, eds_b / 2 + cells + 3 * (size_t)W * 4 + 256, &e));
+  b->tmp = static_cast<uint8_t*>(scratch(ctx, S_AUX, eds_b / 2 + (2 + kIdxSlots) * (size_t)W * 4 + 256, &e));
   b->mask = static_cast<uint8_t*>(scratch(ctx, S_MASK, 2 * cells + 256, &e));
   if (!b->eds || !b->dense || !b->tmp || !b->mask)
     return fail(ctx, CEL_ENOMEM, "device allocation failed");
   b->dmask = b->mask + ((cells + 255) & ~(size_t)255);
   uint8_t* aux = b->tmp + eds_b / 2;
-  b->idx = reinterpret_cast<int32_t*>(aux);
-  b->flags = reinterpret_cast<int32_t*>(aux + (size_t)W * 4);
+  b->flags = reinterpret_cast<int32_t*>(aux);
+  b->idx = reinterpret_cast<int32_t*>(aux + 2 * (size_t)W * 4);
+  const size_t hb = (size_t)kIdxSlots * W * 4 + cells;  // axis-list slots, then the mask
+  if (ctx->hstage_size < hb) {
+    if (ctx->hstage) (void)hipHostFree(ctx->hstage);
+    ctx->hstage = nullptr;
+    ctx->hstage_size = 0;
+    if (hipHostMalloc(&ctx->hstage, hb, hipHostMallocDefault) != hipSuccess)
+      return fail(ctx, CEL_ENOMEM, "page-locked allocation failed");
+    ctx->hstage_size = hb;
+  }
+  b->hidx = static_cast<int32_t*>(ctx->hstage);
+  b->hmask = static_cast<uint8_t*>(ctx->hstage) + (size_t)kIdxSlots * W * 4;
+  b->slot = 0;
   return CEL_OK;
 }
 
@@ -1089,7 +1127,7 @@ cel_status cel_repair(cel_ctx* ctx, uint8_t* eds, uint8_t* present, uint32_t k, 
   hipStream_t s = ctx->stream;
   hipError_t e;
   std::vector<uint8_t> hm(cells);
-  for (size_t i = 0; i < cells; i++) hm[i] = present[i] ? 1 : 0;
+  for (size_t i = 0; i < cells; i++) hm[i] = present[i] != 0;
   if ((e = hipMemcpyAsync(b.eds, eds, eds_b, hipMemcpyHostToDevice, s)) != hipSuccess) return hip_fail(ctx, e, "H2D");
   st = repair_core(ctx, b, hm, k, row_roots, col_roots, RepairOut{bad_axis, bad_index, byz_shares, byz_present});
   if (st != CEL_OK && st != CEL_EBYZANTINE && st != CEL_EBADROOT && st != CEL_EUNREPAIRABLE) return st;
@@ -1116,7 +1154,7 @@ cel_status cel_dev_repair(cel_ctx* ctx, void* d_eds, uint8_t* present, uint32_t 
   b.eds = static_cast<uint8_t*>(d_eds);
   if ((st = repair_bufs(ctx, k, false, &b)) != CEL_OK) return st;
   std::vector<uint8_t> hm(cells);
-  for (size_t i = 0; i < cells; i++) hm[i] = present[i] ? 1 : 0;
+  for (size_t i = 0; i < cells; i++) hm[i] = present[i] != 0;
   st = repair_core(ctx, b, hm, k, row_roots, col_roots, RepairOut{bad_axis, bad_index, byz_shares, byz_present});
   if (st == CEL_OK || st == CEL_EBYZANTINE || st == CEL_EBADROOT || st == CEL_EUNREPAIRABLE)
     std::memcpy(present, hm.data(), cells);

@@ -167,4 +167,7 @@ struct cel_ctx {
   // Grow-only device scratch (reused across calls on this ctx).
   void* scratch[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   size_t scratch_size[6] = {0, 0, 0, 0, 0, 0};
+  // Grow-only page-locked host staging (the repair's axis lists).
+  void* hstage = nullptr;
+  size_t hstage_size = 0;
 };

@@ -409,14 +409,16 @@ __device__ void decode_chunk_gf8p(uint32_t* lds, const uint32_t* err, const uint
   const uint32_t n = 2 * m;
   const uint32_t lgn = 31u - __builtin_clz(n);
   constexpr uint32_t U = 16;  // dwords per 64-byte chunk
-  auto tab = [](const uint32_t* t) { return PermTab{t[0], t[1], t[2], t[3], t[4]}; };
-  // x ^= c(idx) * y, skipped for the zero twiddle
-  auto mad = [&](uint32_t& x, uint32_t y, uint32_t idx) {
-    if (c_gf8.skew[idx] != 255u) x ^= gf8_mul4(y, tab(ltw + idx * 5));
+  // a table is 8 dwords in LDS (5 used): one ds_read_b128 + one ds_read_b32
+  auto tab = [](const uint32_t* t) {
+    const uint4 a = *reinterpret_cast<const uint4*>(t);
+    return PermTab{a.x, a.y, a.z, a.w, t[4]};
   };
+  // x ^= c(idx) * y; the zero twiddle's table is all zeros, so no branch
+  auto mad = [&](uint32_t& x, uint32_t y, uint32_t idx) { x ^= gf8_mul4(y, tab(ltw + idx * 8)); };
   for (uint32_t it = threadIdx.x; it < n * U; it += blockDim.x) {
     const uint32_t i = it / U, u = it % U;
-    if (pres[i]) lds[i * 16 + u] = gf8_mul4(lds[i * 16 + u], tab(lmul + err[i] * 5));
+    if (pres[i]) lds[i * 16 + u] = gf8_mul4(lds[i * 16 + u], tab(lmul + err[i] * 8));
   }
   __syncthreads();
   // IFFT (offset 0): layers D = 1, 2, 4, ...; butterfly y ^= x; x ^= c*y
@@ -504,7 +506,7 @@ __device__ void decode_chunk_gf8p(uint32_t* lds, const uint32_t* err, const uint
   }
   for (uint32_t it = threadIdx.x; it < n * U; it += blockDim.x) {
     const uint32_t i = it / U, u = it % U;
-    if (!pres[i]) lds[i * 16 + u] = gf8_mul4(lds[i * 16 + u], tab(lmul + ((255u - err[i]) % 255u) * 5));
+    if (!pres[i]) lds[i * 16 + u] = gf8_mul4(lds[i * 16 + u], tab(lmul + ((255u - err[i]) % 255u) * 8));
   }
   __syncthreads();
 }
@@ -522,11 +524,13 @@ __global__ __launch_bounds__(256) void k_rs_decode(uint8_t* shards, const uint8_
   const uint32_t n = 2 * m;
   uint32_t* err = lds + n * 16;
   uint32_t* ltw = err + 2 * n;      // (err + n: n words of error-locator scratch)
-  uint32_t* lmul = ltw + 255 * 5;   // GF(2^8): [255][5] twiddle tables, [256][5] by log value
-  uint8_t* pres = reinterpret_cast<uint8_t*>(GF16 ? ltw : lmul + 256 * 5);
+  uint32_t* lmul = ltw + 256 * 8;   // GF(2^8): [255][8] twiddle tables, [256][8] by log value (16-B aligned)
+  uint8_t* pres = reinterpret_cast<uint8_t*>(GF16 ? ltw : lmul + 256 * 8);
   if (!GF16) {
-    for (uint32_t i = threadIdx.x; i < 255 * 5; i += blockDim.x) ltw[i] = tw8[(i / 5) * 8 + i % 5];
-    for (uint32_t i = threadIdx.x; i < 256 * 5; i += blockDim.x) lmul[i] = mul8[(i / 5) * 8 + i % 5];
+    for (uint32_t i = threadIdx.x; i < 255 * 2; i += blockDim.x)
+      reinterpret_cast<uint4*>(ltw)[i] = reinterpret_cast<const uint4*>(tw8)[i];
+    for (uint32_t i = threadIdx.x; i < 256 * 2; i += blockDim.x)
+      reinterpret_cast<uint4*>(lmul)[i] = reinterpret_cast<const uint4*>(mul8)[i];
   }
   __shared__ uint8_t s_log[256];
   uint8_t* axis = shards + (uint64_t)blockIdx.x * n * len;
@@ -612,7 +616,7 @@ hipError_t launch_rs_decode(uint8_t* shards, const uint8_t* present, uint32_t na
   hipError_t e = ensure_gf8_const();
   if (e != hipSuccess) return e;
   const uint32_t n = 2 * m;
-  const size_t lds = (size_t)n * 64 + (size_t)n * 8 + n + (2 * m <= 256 ? (255 + 256) * 5 * 4 : 0);
+  const size_t lds = (size_t)n * 64 + (size_t)n * 8 + n + (2 * m <= 256 ? (256 + 256) * 8 * 4 : 0);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   // 2 chunks per workgroup: the per-axis setup (error locator, table staging) is shared
   // by both 64-byte chunks (1 and 4 measured slower, profiles/r1j_repair_cpw_ab.txt)
