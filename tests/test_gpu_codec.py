@@ -48,6 +48,20 @@ def test_decode_random_erasures(ctx, oracle, n):
         assert np.array_equal(np.frombuffer(b"".join(out), np.uint8).reshape(2 * n, ln), cw)
 
 
+@pytest.mark.parametrize("n,ln", [(16, 64), (128, 64), (128, 192), (64, 320)])
+def test_decode_chunk_tails(ctx, oracle, n, ln):
+    """GF(2^8) decode works on 128-byte chunks; shard sizes that end in a 64-byte half
+    chunk (zero-padded columns) decode like any other."""
+    from celestia_eds.rsmt2d import LeoRSCodec
+    codec = LeoRSCodec(ctx)
+    rng = np.random.default_rng(1000 + n + ln)
+    data = rng.integers(0, 256, (n, ln), dtype=np.uint8)
+    cw = np.concatenate([data, oracle.rs_encode(data)])
+    lost = set(rng.choice(2 * n, n, replace=False).tolist())
+    out = codec.Decode([None if i in lost else cw[i].tobytes() for i in range(2 * n)])
+    assert np.array_equal(np.frombuffer(b"".join(out), np.uint8).reshape(2 * n, ln), cw)
+
+
 def test_decode_too_few(ctx):
     from celestia_eds import CelError, _lib
     from celestia_eds.rsmt2d import LeoRSCodec
