@@ -404,10 +404,32 @@ __device__ void decode_chunk(const Ops& ops, uint32_t* lds, uint32_t* err, const
 // Layers go two at a time (radix 4: a thread owns one dword of four points, half the
 // LDS round trips and barriers of radix 2); the formal derivative reads every source
 // before one barrier and writes after it.
-__device__ void decode_chunk_gf8p(uint32_t* lds, const uint32_t* err, const uint8_t* pres, uint32_t m,
-                                  const uint32_t* ltw, const uint32_t* lmul) {
-  const uint32_t n = 2 * m;
-  const uint32_t lgn = 31u - __builtin_clz(n);
+// Compile-time loop: f(std::integral_constant<uint32_t, 0>) .. f(..., N - 1>).
+template <uint32_t N, uint32_t I = 0, class F>
+__device__ __forceinline__ void sfor_u(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<uint32_t, I>{});
+    sfor_u<N, I + 1>(f);
+  }
+}
+
+// Items [0, C) of a 256-thread workgroup, unrolled (C compile-time): item it goes to
+// thread it % 256. A fixed trip count lets the compiler issue all of a thread's LDS loads
+// of a layer before its multiplies (the decode is latency-bound: barriered layers).
+template <uint32_t C, class F>
+__device__ __forceinline__ void for_items(F&& f) {
+#pragma unroll
+  for (uint32_t r = 0; r < (C + 255) / 256; r++) {
+    const uint32_t it = threadIdx.x + 256u * r;
+    if (C % 256 == 0 || it < C) f(it);
+  }
+}
+
+template <uint32_t N>
+__device__ void decode_chunk_gf8p(uint32_t* lds, const uint32_t* err, const uint8_t* pres, const uint32_t* ltw,
+                                  const uint32_t* lmul) {
+  constexpr uint32_t n = N;
+  constexpr uint32_t lgn = __builtin_ctz(N);
   constexpr uint32_t U = 16;  // dwords per 64-byte chunk
   // a table is 8 dwords in LDS (5 used): one ds_read_b128 + one ds_read_b32
   auto tab = [](const uint32_t* t) {
@@ -416,16 +438,15 @@ __device__ void decode_chunk_gf8p(uint32_t* lds, const uint32_t* err, const uint
   };
   // x ^= c(idx) * y; the zero twiddle's table is all zeros, so no branch
   auto mad = [&](uint32_t& x, uint32_t y, uint32_t idx) { x ^= gf8_mul4(y, tab(ltw + idx * 8)); };
-  for (uint32_t it = threadIdx.x; it < n * U; it += blockDim.x) {
+  for_items<n * U>([&](uint32_t it) {
     const uint32_t i = it / U, u = it % U;
     if (pres[i]) lds[i * 16 + u] = gf8_mul4(lds[i * 16 + u], tab(lmul + err[i] * 8));
-  }
+  });
   __syncthreads();
   // IFFT (offset 0): layers D = 1, 2, 4, ...; butterfly y ^= x; x ^= c*y
-  uint32_t lD = 0;
-  for (; lD + 1 < lgn; lD += 2) {
-    const uint32_t D = 1u << lD;
-    for (uint32_t it = threadIdx.x; it < (n / 4) * U; it += blockDim.x) {
+  sfor_u<lgn / 2>([&](auto li) {
+    constexpr uint32_t lD = 2 * decltype(li)::value, D = 1u << lD;
+    for_items<(n / 4) * U>([&](uint32_t it) {
       const uint32_t q = it / U, u = it % U;
       const uint32_t b4 = (q >> lD) << (lD + 2), a = b4 + (q & (D - 1));
       uint32_t* p = lds + a * 16 + u;
@@ -435,12 +456,12 @@ __device__ void decode_chunk_gf8p(uint32_t* lds, const uint32_t* err, const uint
       v2 ^= v0; mad(v0, v2, b4 + 2 * D - 1);
       v3 ^= v1; mad(v1, v3, b4 + 2 * D - 1);
       p[0] = v0; p[D * 16] = v1; p[2 * D * 16] = v2; p[3 * D * 16] = v3;
-    }
+    });
     __syncthreads();
-  }
-  if (lD < lgn) {  // odd log2(n): one radix-2 layer left
-    const uint32_t D = 1u << lD;
-    for (uint32_t it = threadIdx.x; it < (n / 2) * U; it += blockDim.x) {
+  });
+  if constexpr (lgn & 1) {  // odd log2(n): one radix-2 layer left
+    constexpr uint32_t lD = lgn - 1, D = 1u << lD;
+    for_items<(n / 2) * U>([&](uint32_t it) {
       const uint32_t pair = it / U, u = it % U;
       const uint32_t base = (pair >> lD) << (lD + 1), a = base + (pair & (D - 1));
       uint32_t x = lds[a * 16 + u], y = lds[(a + D) * 16 + u];
@@ -448,36 +469,35 @@ __device__ void decode_chunk_gf8p(uint32_t* lds, const uint32_t* err, const uint
       mad(x, y, base + D - 1);
       lds[a * 16 + u] = x;
       lds[(a + D) * 16 + u] = y;
-    }
+    });
     __syncthreads();
   }
   {  // formal derivative: new[x] = old[x] ^ xor_{t: bit t of x clear, x + 2^t < n} old[x + 2^t]
-    constexpr uint32_t kMaxItems = 256 * 16 / 256;  // GF(2^8): n <= 256 points, 256 threads
-    uint32_t acc[kMaxItems];
+    constexpr uint32_t kItems = (n * U + 255) / 256;
+    uint32_t acc[kItems];
 #pragma unroll
-    for (uint32_t r = 0; r < kMaxItems; r++) {
+    for (uint32_t r = 0; r < kItems; r++) {
       const uint32_t it = threadIdx.x + r * 256u;
       acc[r] = 0;
-      if (it < n * U) {
+      if ((n * U) % 256 == 0 || it < n * U) {
         const uint32_t x = it / U, u = it % U;
+#pragma unroll
         for (uint32_t t = 1; t < n; t <<= 1)
           if ((x & t) == 0 && x + t < n) acc[r] ^= lds[(x + t) * 16 + u];
       }
     }
     __syncthreads();
 #pragma unroll
-    for (uint32_t r = 0; r < kMaxItems; r++) {
+    for (uint32_t r = 0; r < kItems; r++) {
       const uint32_t it = threadIdx.x + r * 256u;
-      if (it < n * U) lds[(it / U) * 16 + it % U] ^= acc[r];
+      if ((n * U) % 256 == 0 || it < n * U) lds[(it / U) * 16 + it % U] ^= acc[r];
     }
     __syncthreads();
   }
   // FFT: layers D = n/2, ..., 1; butterfly x ^= c*y; y ^= x
-  lD = lgn;
-  if (lgn & 1) {  // odd log2(n): the top layer alone
-    lD = lgn - 1;
-    const uint32_t D = 1u << lD;
-    for (uint32_t it = threadIdx.x; it < (n / 2) * U; it += blockDim.x) {
+  if constexpr (lgn & 1) {  // odd log2(n): the top layer alone
+    constexpr uint32_t lD = lgn - 1, D = 1u << lD;
+    for_items<(n / 2) * U>([&](uint32_t it) {
       const uint32_t pair = it / U, u = it % U;
       const uint32_t base = (pair >> lD) << (lD + 1), a = base + (pair & (D - 1));
       uint32_t x = lds[a * 16 + u], y = lds[(a + D) * 16 + u];
@@ -485,13 +505,12 @@ __device__ void decode_chunk_gf8p(uint32_t* lds, const uint32_t* err, const uint
       y ^= x;
       lds[a * 16 + u] = x;
       lds[(a + D) * 16 + u] = y;
-    }
+    });
     __syncthreads();
   }
-  while (lD >= 2) {
-    lD -= 2;  // layers 2D then D
-    const uint32_t D = 1u << lD;
-    for (uint32_t it = threadIdx.x; it < (n / 4) * U; it += blockDim.x) {
+  sfor_u<lgn / 2>([&](auto li) {
+    constexpr uint32_t lD = 2 * (lgn / 2 - 1 - decltype(li)::value), D = 1u << lD;  // layers 2D then D
+    for_items<(n / 4) * U>([&](uint32_t it) {
       const uint32_t q = it / U, u = it % U;
       const uint32_t b4 = (q >> lD) << (lD + 2), a = b4 + (q & (D - 1));
       uint32_t* p = lds + a * 16 + u;
@@ -501,19 +520,19 @@ __device__ void decode_chunk_gf8p(uint32_t* lds, const uint32_t* err, const uint
       mad(v0, v1, b4 + D - 1); v1 ^= v0;
       mad(v2, v3, b4 + 3 * D - 1); v3 ^= v2;
       p[0] = v0; p[D * 16] = v1; p[2 * D * 16] = v2; p[3 * D * 16] = v3;
-    }
+    });
     __syncthreads();
-  }
-  for (uint32_t it = threadIdx.x; it < n * U; it += blockDim.x) {
+  });
+  for_items<n * U>([&](uint32_t it) {
     const uint32_t i = it / U, u = it % U;
     if (!pres[i]) lds[i * 16 + u] = gf8_mul4(lds[i * 16 + u], tab(lmul + ((255u - err[i]) % 255u) * 8));
-  }
+  });
   __syncthreads();
 }
 
 // grid: x = axis, y = 64-byte chunk. shards: [naxes][2m][len] in rsmt2d order
 // (data then parity); present: [naxes][2m].
-template <bool GF16>
+template <bool GF16, uint32_t N8>
 __global__ __launch_bounds__(256) void k_rs_decode(uint8_t* shards, const uint8_t* present, uint32_t m,
                                                    uint32_t len, const uint16_t* __restrict__ gexp,
                                                    const uint16_t* __restrict__ glog,
@@ -597,7 +616,7 @@ __global__ __launch_bounds__(256) void k_rs_decode(uint8_t* shards, const uint8_
       Gf16Ops ops{gexp, glog};
       decode_chunk(ops, lds, err, pres, m, [&](uint32_t i) { return (uint32_t)gskew[i]; });
     } else {
-      decode_chunk_gf8p(lds, err, pres, m, ltw, lmul);
+      if constexpr (N8 != 0) decode_chunk_gf8p<N8>(lds, err, pres, ltw, lmul);
     }
     for (uint32_t it = threadIdx.x; it < n * 4; it += blockDim.x) {
       const uint32_t p = it >> 2, q = it & 3;
@@ -623,16 +642,23 @@ hipError_t launch_rs_decode(uint8_t* shards, const uint8_t* present, uint32_t na
   constexpr uint32_t cpw = 2;
   const uint32_t nch = len / 64;
   dim3 grid(naxes, (nch + cpw - 1) / cpw);
-  if (lds > 64 * 1024) {
-    (void)hipFuncSetAttribute((const void*)k_rs_decode<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    (void)hipFuncSetAttribute((const void*)k_rs_decode<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  auto go = [&](auto kern) {
+    if (lds > 64 * 1024)
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, shards, present, m, len, t.exp16, t.log16, t.skew16, t.tw8,
+                       t.mul8);
+  };
+  switch (n) {  // GF(2^8): the point count is a template constant (unrolled layers)
+    case 2: go(k_rs_decode<false, 2>); break;
+    case 4: go(k_rs_decode<false, 4>); break;
+    case 8: go(k_rs_decode<false, 8>); break;
+    case 16: go(k_rs_decode<false, 16>); break;
+    case 32: go(k_rs_decode<false, 32>); break;
+    case 64: go(k_rs_decode<false, 64>); break;
+    case 128: go(k_rs_decode<false, 128>); break;
+    case 256: go(k_rs_decode<false, 256>); break;
+    default: go(k_rs_decode<true, 0>); break;
   }
-  if (2 * m <= 256)
-    hipLaunchKernelGGL(k_rs_decode<false>, grid, dim3(256), lds, s, shards, present, m, len, t.exp16, t.log16,
-                       t.skew16, t.tw8, t.mul8);
-  else
-    hipLaunchKernelGGL(k_rs_decode<true>, grid, dim3(256), lds, s, shards, present, m, len, t.exp16, t.log16,
-                       t.skew16, t.tw8, t.mul8);
   return hipGetLastError();
 }
 
