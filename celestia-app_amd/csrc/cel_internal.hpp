@@ -148,6 +148,10 @@ hipError_t launch_commitment(const uint8_t* d_cells, uint32_t k, uint32_t r0, ui
 hipError_t launch_rs_decode(uint8_t* shards, const uint8_t* present, uint32_t naxes, uint32_t n,
                             uint32_t len, const DeviceTables& t, void* work, hipStream_t s);
 size_t decode_workspace_size(uint32_t naxes, uint32_t n);
+// GF(2^8) register-resident decode (rs_decode_axis.hip): n = 32..256 points, len % 64 == 0.
+bool rs_decode_axis_supported(uint32_t n, uint32_t len);
+hipError_t launch_rs_decode_axis(uint8_t* shards, const uint8_t* present, uint32_t naxes, uint32_t n, uint32_t len,
+                                 const uint32_t* mul8, hipStream_t s);
 
 }  // namespace cel
 

@@ -648,6 +648,7 @@ hipError_t launch_rs_decode(uint8_t* shards, const uint8_t* present, uint32_t na
     hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, shards, present, m, len, t.exp16, t.log16, t.skew16, t.tw8,
                        t.mul8);
   };
+  if (rs_decode_axis_supported(n, len)) return launch_rs_decode_axis(shards, present, naxes, n, len, t.mul8, s);
   switch (n) {  // GF(2^8): the point count is a template constant (unrolled layers)
     case 2: go(k_rs_decode<false, 2>); break;
     case 4: go(k_rs_decode<false, 4>); break;
