@@ -286,10 +286,11 @@ def run_repair(a):
     resident in HBM (cel_dev_repair); the fresh damaged copy each step needs is made
     before the step's clock starts. host: host buffers in and out (cel_repair), PCIe
     copies included. Single rank.
-    roofline: k_rs_decode alone (cel_dev_decode over the row pass's axes of the same
-    mask), algorithmic bytes = every shard of every decoded axis read once + every
-    missing shard written once, against HBM; the decoder is VALU/LDS-bound (its twiddle
-    tables come from LDS per butterfly), so the fraction says how far from streaming."""
+    roofline: the decoder alone (cel_dev_decode over the row pass's axes of the same
+    mask: k_rs_decode_axis, register-resident GF(2^8)), algorithmic bytes = every shard of
+    every decoded axis read once + every missing shard written once, against HBM; the
+    decoder is VALU-bound (~15K VALU per wave, one wave per SIMD at 239 axes), so the
+    fraction says how far from streaming."""
     torch.cuda.set_device(0)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
@@ -385,7 +386,7 @@ def run_repair(a):
                                   else "(EDS resident in HBM; the damaged-copy restore runs before each step's "
                                        "clock)"),
                    "k": k, "parallelism": "single"},
-        "roofline": {"bound": "hbm", "kernel": "k_rs_decode (cel_dev_decode, the row pass's axes)",
+        "roofline": {"bound": "hbm", "kernel": "k_rs_decode_axis (cel_dev_decode, the row pass's axes)",
                      "achieved": dec_bytes / t_dec / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": dec_bytes / t_dec / 1e9 / HBM_PEAK_GBS, "traffic": None,
                      "avg_launch_us": t_dec * 1e6, "axes": len(rows),

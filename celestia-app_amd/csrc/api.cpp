@@ -887,7 +887,6 @@ struct Check {
 struct Solve {
   int is_col;
   int32_t idx;
-  size_t before;  // offset of the axis's presence mask before the solve (W bytes) in the log
 };
 
 struct RepairOut {
@@ -897,11 +896,86 @@ struct RepairOut {
   uint8_t* byz_present;  // nullable, W
 };
 
+// a[i] bit j <-> a[j] bit i
+static void transpose64(uint64_t* a) {
+  uint64_t m = 0x00000000FFFFFFFFull;
+  for (int j = 32; j != 0; j >>= 1, m ^= (m << j)) {
+    for (int k = 0; k < 64; k = ((k | j) + 1) & ~j) {
+      const uint64_t t = ((a[k] >> j) ^ a[k | j]) & m;
+      a[k | j] ^= t;
+      a[k] ^= t << j;
+    }
+  }
+}
+
+// The presence mask as bitsets by row and by column (bit j of axis i = cell j of it) with
+// per-axis counts, so a solve's bookkeeping visits only the cells it fills.
+struct MaskBits {
+  uint32_t W, nw;
+  std::vector<uint64_t> bits[2];  // [is_col][axis * nw + word]
+  std::vector<uint32_t> cnt[2];
+  uint64_t total = 0;
+  MaskBits(const std::vector<uint8_t>& hm, uint32_t w) : W(w), nw((w + 63) / 64) {
+    const uint32_t P = nw * 64;  // padded to whole 64x64 tiles for the transpose
+    std::vector<uint64_t> rows((size_t)P * nw, 0), cols((size_t)P * nw, 0);
+    for (uint32_t i = 0; i < W; i++) {
+      const uint8_t* r = hm.data() + (size_t)i * W;
+      for (uint32_t j = 0; j < W; j += 8) {
+        uint64_t x = 0;
+        const uint32_t n = W - j < 8 ? W - j : 8;
+        std::memcpy(&x, r + j, n);  // bytes 0 / 1
+        rows[(size_t)i * nw + j / 64] |= ((x * 0x0102040810204080ull) >> 56) << (j % 64);
+      }
+    }
+    // cols = rows transposed, tile by tile
+    uint64_t t[64];
+    for (uint32_t bi = 0; bi < nw; bi++)
+      for (uint32_t bj = 0; bj < nw; bj++) {
+        for (int r = 0; r < 64; r++) t[r] = rows[(size_t)(bi * 64 + r) * nw + bj];
+        transpose64(t);
+        for (int r = 0; r < 64; r++) cols[(size_t)(bj * 64 + r) * nw + bi] = t[r];
+      }
+    rows.resize((size_t)W * nw);
+    cols.resize((size_t)W * nw);
+    bits[0] = std::move(rows);
+    bits[1] = std::move(cols);
+    for (int d = 0; d < 2; d++) {
+      cnt[d].assign(W, 0);
+      for (uint32_t i = 0; i < W; i++) {
+        uint32_t c = 0;
+        for (uint32_t q = 0; q < nw; q++) c += (uint32_t)__builtin_popcountll(bits[d][(size_t)i * nw + q]);
+        cnt[d][i] = c;
+      }
+    }
+    for (uint32_t i = 0; i < W; i++) total += cnt[0][i];
+  }
+  // axis (is_col, i) gets all its cells; appends each orthogonal axis this completes to
+  // done, in ascending order
+  void fill(int is_col, uint32_t i, std::vector<int32_t>& done) {
+    uint64_t* a = bits[is_col].data() + (size_t)i * nw;
+    const uint64_t bit = 1ull << (i % 64);
+    for (uint32_t q = 0; q < nw; q++) {
+      const uint64_t valid = (q + 1) * 64 <= W ? ~0ull : ((1ull << (W % 64)) - 1);
+      uint64_t miss = ~a[q] & valid;
+      a[q] = valid;
+      while (miss) {
+        const uint32_t j = q * 64 + (uint32_t)__builtin_ctzll(miss);
+        miss &= miss - 1;
+        bits[!is_col][(size_t)j * nw + i / 64] |= bit;
+        total++;
+        if (++cnt[!is_col][j] == W) done.push_back((int32_t)j);
+      }
+    }
+    cnt[is_col][i] = W;
+  }
+};
+
 // rsmt2d Repair over the EDS resident at b.eds. hm = host presence mask (updated: all
-// ones on success, the mask before the failing solve on a byzantine / bad-root error).
-// No pass waits for the device. Root checks are deferred: an axis, once complete, never
-// changes, so one commit pass over the final square gives every root rsmt2d checks on
-// the way, and the checks are replayed in rsmt2d's order, reporting the first failure.
+// ones on success, the mask before the failing solve on a byzantine / bad-root error,
+// the mask after the last solve when stuck). No pass waits for the device. Root checks
+// are deferred: an axis, once complete, never changes, so one commit pass over the final
+// square gives every root rsmt2d checks on the way, and the checks are replayed in
+// rsmt2d's order, reporting the first failure.
 static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>& hm, uint32_t k,
                               const uint8_t* row_roots, const uint8_t* col_roots, const RepairOut& out) {
   const uint32_t W = 2 * k;
@@ -913,84 +987,50 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
   if ((e = hipMemcpyAsync(b.mask, b.hmask, cells, hipMemcpyHostToDevice, s)) != hipSuccess ||
       (e = hipMemsetAsync(b.flags, 0, 2 * (size_t)W * 4, s)) != hipSuccess)
     return hip_fail(ctx, e, "H2D");
-  const std::vector<uint8_t> initial = hm;
-  auto at = [&](int is_col, uint32_t i, uint32_t j) -> uint8_t& {
-    return is_col ? hm[(size_t)j * W + i] : hm[(size_t)i * W + j];
-  };
-  std::vector<uint32_t> cnt[2] = {std::vector<uint32_t>(W, 0), std::vector<uint32_t>(W, 0)};  // known cells per axis
-  for (uint32_t i = 0; i < W; i++) {  // hm holds 0/1: plain sums (vectorised)
-    const uint8_t* row = hm.data() + (size_t)i * W;
-    uint32_t c = 0;
-    for (uint32_t j = 0; j < W; j++) {
-      c += row[j];
-      cnt[1][j] += row[j];
-    }
-    cnt[0][i] = c;
-  }
-  auto count = [&](int is_col, uint32_t i) { return cnt[is_col][i]; };
+  MaskBits mb(hm, W);
   std::vector<Check> order;
   std::vector<Solve> solves;
-  std::vector<uint8_t> befores;  // presence masks of the solved axes before their solves
-  std::vector<std::vector<int32_t>> lists;  // kept alive until the final sync
   // preRepairSanityCheck: for i: row i, column i
   {
     std::vector<int32_t> comp[2];
     for (uint32_t i = 0; i < W; i++)
       for (int is_col = 0; is_col < 2; is_col++)
-        if (count(is_col, i) == W) {
+        if (mb.cnt[is_col][i] == W) {
           order.push_back({Check::SANITY, is_col, (int32_t)i, -1});
           comp[is_col].push_back((int32_t)i);
         }
-    for (int is_col = 0; is_col < 2; is_col++) {
+    for (int is_col = 0; is_col < 2; is_col++)
       if ((st = axes_pass(ctx, b, k, is_col, comp[is_col], false)) != CEL_OK) return st;
-      lists.push_back(std::move(comp[is_col]));
-    }
   }
   // solveCrossword: all rows, then all columns, until solved or stuck
   bool solved = false;
+  std::vector<int32_t> list, orth;
   for (;;) {
     bool progress = false;
     for (int is_col = 0; is_col < 2; is_col++) {
-      std::vector<int32_t> list, orth;
+      list.clear();
+      orth.clear();
       for (uint32_t i = 0; i < W; i++) {
-        const uint32_t c = count(is_col, i);
+        const uint32_t c = mb.cnt[is_col][i];
         if (c >= k && c < W) list.push_back((int32_t)i);
       }
       if (list.empty()) continue;
       if ((st = axes_pass(ctx, b, k, is_col, list, true)) != CEL_OK) return st;
       // sequential view of the pass: solve i fills its missing cells, completing the
       // orthogonal axes whose only missing cell it was
-      befores.reserve(befores.size() + list.size() * W);
       for (int32_t i : list) {
-        const Solve sv{is_col, i, befores.size()};
-        befores.resize(befores.size() + W);
-        uint8_t* bf = befores.data() + sv.before;
-        if (is_col)
-          for (uint32_t j = 0; j < W; j++) bf[j] = hm[(size_t)j * W + (uint32_t)i];
-        else
-          std::memcpy(bf, hm.data() + (size_t)i * W, W);
         const int32_t si = (int32_t)solves.size();
         order.push_back({Check::SOLVE, is_col, i, si});
-        for (uint32_t j = 0; j < W; j++) {
-          if (bf[j]) continue;
-          at(is_col, (uint32_t)i, j) = 1;
-          cnt[is_col][i]++;
-          if (++cnt[!is_col][j] == W) {
-            order.push_back({Check::ORTH, !is_col, (int32_t)j, si});
-            orth.push_back((int32_t)j);
-          }
-        }
-        solves.push_back(sv);
+        const size_t o0 = orth.size();
+        mb.fill(is_col, (uint32_t)i, orth);
+        for (size_t t = o0; t < orth.size(); t++) order.push_back({Check::ORTH, !is_col, orth[t], si});
+        solves.push_back({is_col, i});
       }
       std::sort(orth.begin(), orth.end());
       if ((st = axes_pass(ctx, b, k, !is_col, orth, false)) != CEL_OK) return st;
-      lists.push_back(std::move(list));
-      lists.push_back(std::move(orth));
       progress = true;
     }
-    size_t have = 0;
-    for (uint32_t i = 0; i < W; i++) have += cnt[0][i];
-    if (have == cells) {
+    if (mb.total == cells) {
       solved = true;
       break;
     }
@@ -1013,18 +1053,23 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
     return std::memcmp(got.data() + is_col * roots_b + (size_t)i * kNode, exp, kNode) == 0;
   };
   auto enc_ok = [&](int is_col, int32_t i) { return flags[(size_t)is_col * W + i] == 0; };
-  // the presence mask before solve `upto` (all solves before it applied)
-  auto rollback = [&](int32_t upto) {
-    hm = initial;
-    for (int32_t t = 0; t < upto; t++)
-      for (uint32_t j = 0; j < W; j++) at(solves[t].is_col, (uint32_t)solves[t].idx, j) = 1;
+  // hm := the presence mask before solve `upto` (all solves before it applied)
+  auto rollback = [&](size_t upto) {
+    for (size_t t = 0; t < upto; t++) {
+      const uint32_t i = (uint32_t)solves[t].idx;
+      if (solves[t].is_col)
+        for (uint32_t j = 0; j < W; j++) hm[(size_t)j * W + i] = 1;
+      else
+        std::memset(hm.data() + (size_t)i * W, 1, W);
+    }
   };
-  auto fail_axis = [&](cel_status code, int is_col, int32_t idx, const uint8_t* axis_mask) {
+  auto fail_axis = [&](cel_status code, int is_col, int32_t idx, bool masked) {
     if (out.bad_axis) *out.bad_axis = is_col;
     if (out.bad_index) *out.bad_index = idx;
     if (code == CEL_EBYZANTINE && (out.byz_shares || out.byz_present)) {
       // ErrByzantineData.Shares: the axis's cells from the square (complete axes never
-      // change; cells of a solved axis present before its solve kept their bytes)
+      // change; cells of a solved axis present before its solve kept their bytes), with
+      // the axis's mask before its solve (hm is rolled back to it)
       std::vector<uint8_t> axis((size_t)W * kShare);
       const uint8_t* src = b.eds + (is_col ? (size_t)idx * kShare : (size_t)idx * W * kShare);
       const hipError_t ce = is_col ? hipMemcpy2D(axis.data(), kShare, src, (size_t)W * kShare, kShare, W,
@@ -1032,7 +1077,7 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
                                    : hipMemcpy(axis.data(), src, axis.size(), hipMemcpyDeviceToHost);
       if (ce != hipSuccess) return hip_fail(ctx, ce, "byzantine shares");
       for (uint32_t j = 0; j < W; j++) {
-        const uint8_t p = axis_mask ? axis_mask[j] : 1;
+        const uint8_t p = masked ? hm[is_col ? (size_t)j * W + (uint32_t)idx : (size_t)idx * W + j] : 1;
         if (out.byz_present) out.byz_present[j] = p;
         if (out.byz_shares) {
           if (p) std::memcpy(out.byz_shares + (size_t)j * kShare, axis.data() + (size_t)j * kShare, kShare);
@@ -1048,30 +1093,28 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
   for (const Check& c : order) {
     switch (c.kind) {
       case Check::SANITY:
-        if (!root_ok(c.is_col, c.idx)) {
-          rollback(0);
-          return fail_axis(CEL_EBADROOT, c.is_col, c.idx, nullptr);
-        }
-        if (!enc_ok(c.is_col, c.idx)) {
-          rollback(0);
-          return fail_axis(CEL_EBYZANTINE, c.is_col, c.idx, nullptr);
-        }
+        if (!root_ok(c.is_col, c.idx)) return fail_axis(CEL_EBADROOT, c.is_col, c.idx, false);
+        if (!enc_ok(c.is_col, c.idx)) return fail_axis(CEL_EBYZANTINE, c.is_col, c.idx, false);
         break;
       case Check::SOLVE:
         if (!enc_ok(c.is_col, c.idx) || !root_ok(c.is_col, c.idx)) {
-          rollback(c.solve);
-          return fail_axis(CEL_EBYZANTINE, c.is_col, c.idx, befores.data() + solves[c.solve].before);
+          rollback((size_t)c.solve);
+          return fail_axis(CEL_EBYZANTINE, c.is_col, c.idx, true);
         }
         break;
       case Check::ORTH:
         if (!root_ok(c.is_col, c.idx) || !enc_ok(c.is_col, c.idx)) {
-          rollback(c.solve);
-          return fail_axis(CEL_EBYZANTINE, c.is_col, c.idx, nullptr);
+          rollback((size_t)c.solve);
+          return fail_axis(CEL_EBYZANTINE, c.is_col, c.idx, false);
         }
         break;
     }
   }
-  if (!solved) return fail(ctx, CEL_EUNREPAIRABLE, "failed to solve data square");
+  if (!solved) {
+    rollback(solves.size());
+    return fail(ctx, CEL_EUNREPAIRABLE, "failed to solve data square");
+  }
+  std::fill(hm.begin(), hm.end(), (uint8_t)1);
   return CEL_OK;
 }
 

@@ -41,13 +41,37 @@ using cx::sfor;
 
 __constant__ cx::Gf8Tables c_t8 = cx::kGf8;
 
-__device__ __forceinline__ uint32_t perm_mul(uint32_t y, const uint32_t* t) {
-  const uint4 a = *reinterpret_cast<const uint4*>(t);
+// y * c with c's product tables {t0l, t0h, t1l, t1h} in a and t2 in t4 (rs_kernels.hip gf8_mul4)
+__device__ __forceinline__ uint32_t perm_mul(uint32_t y, uint4 a, uint32_t t4) {
   const uint32_t s0 = y & 0x07070707u;
   const uint32_t s1 = (y >> 3) & 0x07070707u;
   const uint32_t s2 = (y >> 6) & 0x03030303u;
   return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_perm(a.y, a.x, s0), __builtin_amdgcn_perm(a.w, a.z, s1),
-                                     __builtin_amdgcn_perm(0u, t[4], s2), 0x96);
+                                     __builtin_amdgcn_perm(0u, t4, s2), 0x96);
+}
+
+// f(r, table of register r) for r = 0 .. R-1, the LDS tables read LA registers ahead of
+// their use (a table per point: register r of this lane half is at t + 16 r dwords)
+template <int R, int LA, class F>
+__device__ __forceinline__ void with_tables(const uint32_t* t, F&& f) {
+  uint4 ta[LA];
+  uint32_t tb[LA];
+  sfor<LA>([&](auto i) {
+    constexpr int r = decltype(i)::value;
+    ta[r] = *reinterpret_cast<const uint4*>(t + 16 * r);
+    tb[r] = t[16 * r + 4];
+  });
+  sfor<R>([&](auto ri) {
+    constexpr int r = decltype(ri)::value;
+    const uint4 a = ta[r % LA];
+    const uint32_t b = tb[r % LA];
+    if constexpr (r + LA < R) {
+      ta[r % LA] = *reinterpret_cast<const uint4*>(t + 16 * (r + LA));
+      tb[r % LA] = t[16 * (r + LA) + 4];
+    }
+    f(std::integral_constant<int, r>{}, a, b);
+    __builtin_amdgcn_sched_barrier(0);
+  });
 }
 
 // Layer D = 1 (pairs (2r, 2r+1) = register r of the two lane halves). After the swap
@@ -156,10 +180,9 @@ __global__ __launch_bounds__(256, 2) void k_rs_decode_axis(uint8_t* __restrict__
 
   const uint32_t m7 = sconst<0x07070707u>(), m3 = sconst<0x03030303u>();
   // scale in: work = shard * exp(err) on present points, 0 on erased ones
-  sfor<R>([&](auto ri) {
+  with_tables<R, 8>(ltab[0][h], [&](auto ri, uint4 a, uint32_t b) {
     constexpr int r = decltype(ri)::value;
-    w[r] = perm_mul(w[r], ltab[0][2 * r + h]);
-    __builtin_amdgcn_sched_barrier(0);
+    w[r] = perm_mul(w[r], a, b);
   });
   // IFFT, skew index base + D - 1
   sfor<R>([&](auto ri) {
@@ -266,16 +289,13 @@ __global__ __launch_bounds__(256, 2) void k_rs_decode_axis(uint8_t* __restrict__
   if (!active) return;
   uint32_t slen = len;  // recomputed shard offsets below (not 128 SGPRs live from the loads)
   asm volatile("" : "+s"(slen));
-  sfor<(R + 31) / 32>([&](auto wi) {
-    constexpr int word = decltype(wi)::value;
-    const uint32_t miss = s_miss[h][word];
-    sfor<(R - 32 * word < 32 ? R - 32 * word : 32)>([&](auto bi) {
-      constexpr int r = 32 * word + decltype(bi)::value;
-      if ((miss >> (r & 31)) & 1u) {
-        const uint32_t v = perm_mul(w[r], ltab[1][2 * r + h]);
-        __builtin_amdgcn_raw_buffer_store_b32(v, rs, vo, (uint32_t)((2 * r) ^ M) * slen, 2);
-      }
-    });
+  uint32_t miss[NW];
+  sfor<NW>([&](auto i) { miss[decltype(i)::value] = s_miss[h][decltype(i)::value]; });
+  with_tables<R, 8>(ltab[1][h], [&](auto ri, uint4 a, uint32_t b) {
+    constexpr int r = decltype(ri)::value;
+    const uint32_t v = perm_mul(w[r], a, b);
+    if ((miss[r / 32] >> (r & 31)) & 1u)
+      __builtin_amdgcn_raw_buffer_store_b32(v, rs, vo, (uint32_t)((2 * r) ^ M) * slen, 2);
   });
 }
 
