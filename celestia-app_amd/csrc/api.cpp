@@ -162,10 +162,10 @@ cel_status cel_device_name(cel_ctx* ctx, char* buf, size_t len) {
 // ------------------------------------------------------------------ squares
 
 // Chunking of a batch over the internal streams: chunk c runs RS extension then NMT +
-// DAH on stream sub[c % kPipe]. Extensions are chained (chunk c+1's starts when chunk
-// c's ends) so each runs on the whole chip while earlier chunks hash: the VALU-bound
-// hashing of chunk c overlaps the extension of chunk c+1, and only the last chunk's
-// latency-bound tree top + DAH is exposed. Two chunks (profiles/r1g_pipe_chunks_ab.txt).
+// DAH on stream sub[c % kPipe]; the chunks start together, so one chunk's latency-bound
+// tree top + DAH runs beside the other's work. Two chunks (profiles/r1g_pipe_chunks_ab.txt);
+// chaining the extensions so each runs beside the previous chunk's hashing buys nothing,
+// the step is the sum of the two VALU-bound phases (profiles/r2_pipe_overlap_ab.txt).
 constexpr uint32_t kPipeChunks = 2;
 
 static void pipe_plan(uint32_t n, uint32_t* chunk, uint32_t* nchunks) {
