@@ -814,46 +814,59 @@ namespace {
 constexpr uint32_t kIdxSlots = 64;
 
 struct RepairBufs {
+  uint32_t W;
   uint8_t* eds;
   uint8_t* mask;
-  uint8_t* dense;
+  uint8_t* dense[2];  // gathered axes of the solve passes, alternating (main stream)
   uint8_t* dmask;
-  uint8_t* tmp;
-  int32_t* idx;    // [kIdxSlots][W] device axis lists
-  int32_t* hidx;   // [kIdxSlots][W] page-locked staging of the same
-  uint8_t* hmask;  // [W][W] page-locked staging of the presence mask
-  uint32_t slot;   // next free slot
-  int32_t* flags;  // [2][W] encoding-check flags by (direction, axis): an axis completes once
+  uint8_t* dchk;      // gathered axes of the check passes (side stream)
+  uint8_t* dmask_chk;
+  uint8_t* tmp;       // re-encoded parity halves (side stream)
+  uint8_t* work;      // NMT workspace of the final verification
+  uint8_t* roots;     // [2][W][90] row then column roots of the final verification, then flags
+  uint8_t* hres;      // page-locked copy of roots + flags (one D2H at the end)
+  size_t res_bytes;
+  int32_t* idx;       // [kIdxSlots][W] device axis lists
+  int32_t* hidx;      // [kIdxSlots][W] page-locked staging of the same
+  uint8_t* hmask;     // [W][W] page-locked staging of the presence mask
+  uint32_t slot;      // next free slot
+  uint32_t solves;    // solve passes so far (which dense buffer is next)
+  int32_t* flags;     // [2][W] encoding-check flags by (direction, axis), right after the roots
+  // Two streams: the solve chain (gather -> decode -> scatter) runs on `main`; every
+  // re-encode check (of the solved axes, the sanity and the orthogonal checks) runs on
+  // `side`, off the chain's critical path: its outcome is only read at the end.
+  hipStream_t main, side;
+  hipEvent_t ev_main;     // the square after the main stream's latest pass
+  hipEvent_t ev_side[2];  // the side stream is done with dense[i]
+  hipEvent_t ev_done;     // the side stream's last check
 };
 
-// Re-encode check of `list` (axes of one direction): the data half of each axis is
-// encoded again and compared with its parity half; mismatches set flags[is_col*W + axis].
-// decode: the axes are incomplete and get decoded first (rsmt2d solveCrossword) and the
-// decoded cells are scattered back into the square; otherwise they are complete already
-// (preRepairSanityCheck, and the orthogonal axes a solve completes). Nothing is
-// synchronised: every flag is read back once at the end of the repair.
-static cel_status axes_pass(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_col, const std::vector<int32_t>& list,
-                            bool decode) {
-  const Range range(decode ? "repair.solve" : "repair.check");
-  const uint32_t W = 2 * k, na = (uint32_t)list.size();
-  if (!na) return CEL_OK;
-  hipStream_t s = ctx->stream;
+// `list` into the next axis-list slot, uploaded on stream s. Every slot in flight: drain
+// both streams (the side stream's compares read the lists too), then reuse.
+static cel_status upload_list(cel_ctx* ctx, RepairBufs& b, const std::vector<int32_t>& list, hipStream_t s,
+                              int32_t** d_list) {
   hipError_t e;
-  if (b.slot == kIdxSlots) {  // every slot in flight: let them drain, then reuse
-    if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "sync");
+  if (b.slot == kIdxSlots) {
+    if ((e = hipStreamSynchronize(b.main)) != hipSuccess || (e = hipStreamSynchronize(b.side)) != hipSuccess)
+      return hip_fail(ctx, e, "sync");
     b.slot = 0;
   }
-  int32_t* hidx = b.hidx + (size_t)b.slot * W;
-  int32_t* idx = b.idx + (size_t)b.slot * W;
+  int32_t* hidx = b.hidx + (size_t)b.slot * b.W;
+  *d_list = b.idx + (size_t)b.slot * b.W;
   b.slot++;
-  std::memcpy(hidx, list.data(), (size_t)na * 4);
-  if ((e = hipMemcpyAsync(idx, hidx, na * 4, hipMemcpyHostToDevice, s)) != hipSuccess) return hip_fail(ctx, e, "H2D");
-  if ((e = launch_gather_axes(b.eds, b.mask, W, idx, is_col, na, b.dense, b.dmask, s)) != hipSuccess)
-    return hip_fail(ctx, e, "gather");
-  if (decode && (e = launch_rs_decode(b.dense, b.dmask, na, k, kShare, ctx->tables, nullptr, s)) != hipSuccess)
-    return hip_fail(ctx, e, "decode");
+  std::memcpy(hidx, list.data(), list.size() * 4);
+  if ((e = hipMemcpyAsync(*d_list, hidx, list.size() * 4, hipMemcpyHostToDevice, s)) != hipSuccess)
+    return hip_fail(ctx, e, "H2D");
+  return CEL_OK;
+}
+
+// Re-encode check of na gathered axes at `dense` on stream s: the data half of each axis
+// is encoded again and compared with its parity half; mismatches set flags[is_col*W + axis].
+static cel_status encode_check(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_col, uint32_t na, const uint8_t* dense,
+                               const int32_t* idx, hipStream_t s) {
+  const uint32_t W = 2 * k;
   RsGeom g{};
-  g.in = b.dense;
+  g.in = dense;
   g.in_sq = (uint64_t)na * W * kShare;
   g.in_axis = (uint64_t)W * kShare;
   g.in_shard = kShare;
@@ -865,13 +878,54 @@ static cel_status axes_pass(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_col,
   g.len = kShare;
   g.axes = na;
   g.nsq = 1;
+  hipError_t e;
   if ((e = launch_rs_encode(g, ctx->tables, s)) != hipSuccess) return hip_fail(ctx, e, "re-encode");
-  if ((e = launch_cmp(b.tmp, (uint64_t)k * kShare, b.dense + (uint64_t)k * kShare, (uint64_t)W * kShare,
+  if ((e = launch_cmp(b.tmp, (uint64_t)k * kShare, dense + (uint64_t)k * kShare, (uint64_t)W * kShare,
                       (uint64_t)k * kShare, na, b.flags + (size_t)is_col * W, s, idx)) != hipSuccess)
     return hip_fail(ctx, e, "compare");
-  if (decode && (e = launch_scatter_axes(b.eds, b.mask, W, idx, is_col, na, b.dense, s)) != hipSuccess)
-    return hip_fail(ctx, e, "scatter");
   return CEL_OK;
+}
+
+// rsmt2d solveCrossword's decode of `list` (incomplete axes of one direction): gathered,
+// decoded and scattered back into the square on the main stream; their encoding check
+// follows on the side stream. Nothing is synchronised: every flag is read back once at
+// the end of the repair.
+static cel_status solve_pass(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_col, const std::vector<int32_t>& list) {
+  const Range range("repair.solve");
+  const uint32_t W = 2 * k, na = (uint32_t)list.size();
+  if (!na) return CEL_OK;
+  const uint32_t d = b.solves++ & 1u;
+  uint8_t* dense = b.dense[d];
+  int32_t* idx;
+  cel_status st;
+  if ((st = upload_list(ctx, b, list, b.main, &idx)) != CEL_OK) return st;
+  hipError_t e;
+  if ((e = hipStreamWaitEvent(b.main, b.ev_side[d], 0)) != hipSuccess ||  // the side stream is done with dense[d]
+      (e = launch_gather_axes(b.eds, b.mask, W, idx, is_col, na, dense, b.dmask, b.main)) != hipSuccess ||
+      (e = launch_rs_decode(dense, b.dmask, na, k, kShare, ctx->tables, nullptr, b.main)) != hipSuccess ||
+      (e = launch_scatter_axes(b.eds, b.mask, W, idx, is_col, na, dense, b.main)) != hipSuccess ||
+      (e = hipEventRecord(b.ev_main, b.main)) != hipSuccess || (e = hipStreamWaitEvent(b.side, b.ev_main, 0)) != hipSuccess)
+    return hip_fail(ctx, e, "solve");
+  if ((st = encode_check(ctx, b, k, is_col, na, dense, idx, b.side)) != CEL_OK) return st;
+  if ((e = hipEventRecord(b.ev_side[d], b.side)) != hipSuccess) return hip_fail(ctx, e, "event");
+  return CEL_OK;
+}
+
+// Encoding check of complete axes (preRepairSanityCheck, and the orthogonal axes a solve
+// completed), on the side stream after the main stream's latest pass.
+static cel_status check_pass(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_col, const std::vector<int32_t>& list) {
+  const Range range("repair.check");
+  const uint32_t W = 2 * k, na = (uint32_t)list.size();
+  if (!na) return CEL_OK;
+  hipError_t e;
+  if ((e = hipEventRecord(b.ev_main, b.main)) != hipSuccess || (e = hipStreamWaitEvent(b.side, b.ev_main, 0)) != hipSuccess)
+    return hip_fail(ctx, e, "event");
+  int32_t* idx;
+  cel_status st;
+  if ((st = upload_list(ctx, b, list, b.side, &idx)) != CEL_OK) return st;
+  if ((e = launch_gather_axes(b.eds, b.mask, W, idx, is_col, na, b.dchk, b.dmask_chk, b.side)) != hipSuccess)
+    return hip_fail(ctx, e, "gather");
+  return encode_check(ctx, b, k, is_col, na, b.dchk, idx, b.side);
 }
 
 // One check of the replay, in rsmt2d's order (oracle/eds.c orc_repair):
@@ -980,13 +1034,25 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
                               const uint8_t* row_roots, const uint8_t* col_roots, const RepairOut& out) {
   const uint32_t W = 2 * k;
   const size_t cells = (size_t)W * W;
-  hipStream_t s = ctx->stream;
+  hipStream_t s = b.main;
   hipError_t e = hipSuccess;
   cel_status st;
   std::memcpy(b.hmask, hm.data(), cells);
   if ((e = hipMemcpyAsync(b.mask, b.hmask, cells, hipMemcpyHostToDevice, s)) != hipSuccess ||
-      (e = hipMemsetAsync(b.flags, 0, 2 * (size_t)W * 4, s)) != hipSuccess)
+      (e = hipMemsetAsync(b.flags, 0, 2 * (size_t)W * 4, s)) != hipSuccess ||
+      (e = hipEventRecord(b.ev_main, s)) != hipSuccess || (e = hipStreamWaitEvent(b.side, b.ev_main, 0)) != hipSuccess)
     return hip_fail(ctx, e, "H2D");
+  // The first row pass goes to the device before the host builds its bookkeeping (the
+  // mask bitsets, the sanity lists), which then runs beside the decode.
+  std::vector<int32_t> list, orth, first;
+  for (uint32_t i = 0; i < W; i++) {
+    const uint8_t* r = hm.data() + (size_t)i * W;
+    uint32_t c = 0;
+    for (uint32_t j = 0; j < W; j++) c += r[j];
+    if (c >= k && c < W) first.push_back((int32_t)i);
+  }
+  if ((st = solve_pass(ctx, b, k, 0, first)) != CEL_OK) return st;
+  bool first_issued = !first.empty();
   MaskBits mb(hm, W);
   std::vector<Check> order;
   std::vector<Solve> solves;
@@ -1000,11 +1066,10 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
           comp[is_col].push_back((int32_t)i);
         }
     for (int is_col = 0; is_col < 2; is_col++)
-      if ((st = axes_pass(ctx, b, k, is_col, comp[is_col], false)) != CEL_OK) return st;
+      if ((st = check_pass(ctx, b, k, is_col, comp[is_col])) != CEL_OK) return st;
   }
   // solveCrossword: all rows, then all columns, until solved or stuck
   bool solved = false;
-  std::vector<int32_t> list, orth;
   for (;;) {
     bool progress = false;
     for (int is_col = 0; is_col < 2; is_col++) {
@@ -1015,7 +1080,11 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
         if (c >= k && c < W) list.push_back((int32_t)i);
       }
       if (list.empty()) continue;
-      if ((st = axes_pass(ctx, b, k, is_col, list, true)) != CEL_OK) return st;
+      if (first_issued) {  // the first row pass (the same list, issued above)
+        first_issued = false;
+      } else if ((st = solve_pass(ctx, b, k, is_col, list)) != CEL_OK) {
+        return st;
+      }
       // sequential view of the pass: solve i fills its missing cells, completing the
       // orthogonal axes whose only missing cell it was
       for (int32_t i : list) {
@@ -1027,7 +1096,7 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
         solves.push_back({is_col, i});
       }
       std::sort(orth.begin(), orth.end());
-      if ((st = axes_pass(ctx, b, k, !is_col, orth, false)) != CEL_OK) return st;
+      if ((st = check_pass(ctx, b, k, !is_col, orth)) != CEL_OK) return st;
       progress = true;
     }
     if (mb.total == cells) {
@@ -1036,21 +1105,23 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
     }
     if (!progress) break;
   }
-  // every root of the (possibly partial) square in one commit pass, roots only
+  // every root of the (possibly partial) square in one commit pass, roots only, beside
+  // the side stream's last checks; then both streams join
   const size_t roots_b = (size_t)W * kNode;
-  uint8_t* d_rr = b.tmp;  // free after the last pass (stream order)
-  uint8_t* d_cr = b.tmp + roots_b;
-  if ((e = launch_commit(b.eds, k, 1, d_rr, d_cr, nullptr, nullptr, b.dense, false, s)) != hipSuccess)
+  uint8_t* d_rr = b.roots;
+  uint8_t* d_cr = b.roots + roots_b;
+  if ((e = launch_commit(b.eds, k, 1, d_rr, d_cr, nullptr, nullptr, b.work, false, s)) != hipSuccess)
     return hip_fail(ctx, e, "roots");
-  std::vector<uint8_t> got(2 * roots_b);
-  std::vector<int32_t> flags(2 * (size_t)W);
-  if ((e = hipMemcpyAsync(got.data(), d_rr, 2 * roots_b, hipMemcpyDeviceToHost, s)) != hipSuccess ||
-      (e = hipMemcpyAsync(flags.data(), b.flags, flags.size() * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+  if ((e = hipEventRecord(b.ev_done, b.side)) != hipSuccess || (e = hipStreamWaitEvent(s, b.ev_done, 0)) != hipSuccess)
+    return hip_fail(ctx, e, "join");
+  if ((e = hipMemcpyAsync(b.hres, b.roots, b.res_bytes, hipMemcpyDeviceToHost, s)) != hipSuccess)
     return hip_fail(ctx, e, "D2H");
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "sync");
+  const uint8_t* got = b.hres;
+  const int32_t* flags = reinterpret_cast<const int32_t*>(b.hres + (b.res_bytes - 2 * (size_t)W * 4));
   auto root_ok = [&](int is_col, int32_t i) {
     const uint8_t* exp = (is_col ? col_roots : row_roots) + (size_t)i * kNode;
-    return std::memcmp(got.data() + is_col * roots_b + (size_t)i * kNode, exp, kNode) == 0;
+    return std::memcmp(got + is_col * roots_b + (size_t)i * kNode, exp, kNode) == 0;
   };
   auto enc_ok = [&](int is_col, int32_t i) { return flags[(size_t)is_col * W + i] == 0; };
   // hm := the presence mask before solve `upto` (all solves before it applied)
@@ -1121,20 +1192,27 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
 static cel_status repair_bufs(cel_ctx* ctx, uint32_t k, bool own_eds, RepairBufs* b) {
   const uint32_t W = 2 * k;
   const size_t cells = (size_t)W * W, eds_b = cells * kShare;
+  const size_t cells_a = (cells + 255) & ~(size_t)255;
   hipError_t e = hipSuccess;
+  b->W = W;
   if (own_eds) b->eds = static_cast<uint8_t*>(scratch(ctx, S_EDS, eds_b, &e));
-  // dense doubles as the commit workspace of the final verification
-  const size_t dense_b = std::max(eds_b, nmt_workspace_size(k, 1));
-  b->dense = static_cast<uint8_t*>(scratch(ctx, S_IN, dense_b, &e));
-  b->tmp = static_cast<uint8_t*>(scratch(ctx, S_AUX, eds_b / 2 + (2 + kIdxSlots) * (size_t)W * 4 + 256, &e));
-  b->mask = static_cast<uint8_t*>(scratch(ctx, S_MASK, 2 * cells + 256, &e));
-  if (!b->eds || !b->dense || !b->tmp || !b->mask)
+  b->dense[0] = static_cast<uint8_t*>(scratch(ctx, S_IN, 3 * eds_b, &e));
+  b->tmp = static_cast<uint8_t*>(scratch(ctx, S_AUX, eds_b / 2 + (size_t)kIdxSlots * W * 4 + 256, &e));
+  b->mask = static_cast<uint8_t*>(scratch(ctx, S_MASK, 3 * cells_a, &e));
+  b->work = static_cast<uint8_t*>(scratch(ctx, S_WORK, nmt_workspace_size(k, 1), &e));
+  const size_t roots_a = (2 * (size_t)W * kNode + 255) & ~(size_t)255;
+  b->res_bytes = roots_a + 2 * (size_t)W * 4;
+  b->roots = static_cast<uint8_t*>(scratch(ctx, S_ROOTS, b->res_bytes, &e));
+  if (!b->eds || !b->dense[0] || !b->tmp || !b->mask || !b->work || !b->roots)
     return fail(ctx, CEL_ENOMEM, "device allocation failed");
-  b->dmask = b->mask + ((cells + 255) & ~(size_t)255);
-  uint8_t* aux = b->tmp + eds_b / 2;
-  b->flags = reinterpret_cast<int32_t*>(aux);
-  b->idx = reinterpret_cast<int32_t*>(aux + 2 * (size_t)W * 4);
-  const size_t hb = (size_t)kIdxSlots * W * 4 + cells;  // axis-list slots, then the mask
+  b->dense[1] = b->dense[0] + eds_b;
+  b->dchk = b->dense[1] + eds_b;
+  b->dmask = b->mask + cells_a;
+  b->dmask_chk = b->dmask + cells_a;
+  b->flags = reinterpret_cast<int32_t*>(b->roots + roots_a);
+  b->idx = reinterpret_cast<int32_t*>(b->tmp + eds_b / 2);
+  const size_t cells_h = (cells + 255) & ~(size_t)255;
+  const size_t hb = (size_t)kIdxSlots * W * 4 + cells_h + b->res_bytes;  // axis lists, mask, results
   if (ctx->hstage_size < hb) {
     if (ctx->hstage) (void)hipHostFree(ctx->hstage);
     ctx->hstage = nullptr;
@@ -1145,7 +1223,19 @@ static cel_status repair_bufs(cel_ctx* ctx, uint32_t k, bool own_eds, RepairBufs
   }
   b->hidx = static_cast<int32_t*>(ctx->hstage);
   b->hmask = static_cast<uint8_t*>(ctx->hstage) + (size_t)kIdxSlots * W * 4;
+  b->hres = b->hmask + cells_h;
   b->slot = 0;
+  b->solves = 0;
+  // the side stream and the events are the batch pipeline's (the ctx lock is held)
+  b->main = ctx->stream;
+  b->side = ctx->sub[0];
+  b->ev_main = ctx->ev_rs[0];
+  b->ev_side[0] = ctx->ev_rs[1];
+  b->ev_side[1] = ctx->ev_rs[2];
+  b->ev_done = ctx->ev_rs[3];
+  // no stale record of an earlier call may gate this one: both streams start from here
+  if ((e = hipEventRecord(b->ev_side[0], b->side)) != hipSuccess || (e = hipEventRecord(b->ev_side[1], b->side)) != hipSuccess)
+    return hip_fail(ctx, e, "event");
   return CEL_OK;
 }
 
