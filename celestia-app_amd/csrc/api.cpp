@@ -900,6 +900,16 @@ static cel_status solve_pass(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_col
   cel_status st;
   if ((st = upload_list(ctx, b, list, b.main, &idx)) != CEL_OK) return st;
   hipError_t e;
+  if (rs_decode_axis_supported(W, kShare)) {
+    // register decoder in place: erased cells straight into the square (no gather /
+    // scatter on the chain); the side stream gathers the completed axes for their check
+    if ((e = launch_rs_decode_in_square(b.eds, b.mask, W, idx, is_col, na, ctx->tables.mul8, b.main)) != hipSuccess ||
+        (e = hipEventRecord(b.ev_main, b.main)) != hipSuccess ||
+        (e = hipStreamWaitEvent(b.side, b.ev_main, 0)) != hipSuccess ||
+        (e = launch_gather_axes(b.eds, b.mask, W, idx, is_col, na, b.dchk, b.dmask_chk, b.side)) != hipSuccess)
+      return hip_fail(ctx, e, "solve");
+    return encode_check(ctx, b, k, is_col, na, b.dchk, idx, b.side);
+  }
   if ((e = hipStreamWaitEvent(b.main, b.ev_side[d], 0)) != hipSuccess ||  // the side stream is done with dense[d]
       (e = launch_gather_axes(b.eds, b.mask, W, idx, is_col, na, dense, b.dmask, b.main)) != hipSuccess ||
       (e = launch_rs_decode(dense, b.dmask, na, k, kShare, ctx->tables, nullptr, b.main)) != hipSuccess ||

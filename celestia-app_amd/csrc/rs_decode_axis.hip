@@ -94,10 +94,16 @@ __device__ __forceinline__ void cross_fft(uint32_t& v, bool hi, uint32_t m7, uin
   v = hi ? (p[1] ^ x) : x;    // y ^= x
 }
 
+// Axis a (blockIdx.x) is either dense (idx == nullptr: shards + a * N * len, shard stride
+// len, presence present[a * N ..]) or axis idx[a] of a W x W square of len-byte cells at
+// `shards` (a row if !is_col, else a column: shard stride len or W * len) with its
+// presence in the square's mask `present`; in-square decodes store the erased cells
+// straight into the square and mark the axis present (the repair's gather and scatter).
 template <int LOGN>
 __global__ __launch_bounds__(256, 2) void k_rs_decode_axis(uint8_t* __restrict__ shards,
-                                                           const uint8_t* __restrict__ present, uint32_t len,
-                                                           const uint32_t* __restrict__ mul8) {
+                                                           uint8_t* __restrict__ present, uint32_t len,
+                                                           const uint32_t* __restrict__ mul8,
+                                                           const int32_t* __restrict__ idx, uint32_t W, int is_col) {
   constexpr int N = 1 << LOGN, R = N / 2, M = N / 2, NB = R / 8, NW = (R + 31) / 32;
   static_assert(LOGN >= 5 && LOGN <= 8, "register decode covers 32..256 points");
   __shared__ __attribute__((aligned(16))) uint32_t ltab[2][N][8];  // [scale in / out][point][table]
@@ -110,25 +116,41 @@ __global__ __launch_bounds__(256, 2) void k_rs_decode_axis(uint8_t* __restrict__
   const uint32_t slice = blockIdx.y * 4u + (tid >> 6);
   const uint32_t col = slice * 128u + (lane & 31u) * 4u;
   const bool active = col < len;
-  uint8_t* axis = shards + (uint64_t)blockIdx.x * N * len;
+  uint8_t* axis;
+  uint8_t* pa;
+  uint32_t sst, pst;  // shard stride (bytes), presence stride
+  if (idx) {
+    const uint32_t ax = (uint32_t)idx[blockIdx.x];
+    axis = shards + (is_col ? (uint64_t)ax * len : (uint64_t)ax * W * len);
+    sst = is_col ? W * len : len;
+    pa = present + (is_col ? (uint64_t)ax : (uint64_t)ax * W);
+    pst = is_col ? W : 1u;
+  } else {
+    axis = shards + (uint64_t)blockIdx.x * N * len;
+    sst = len;
+    pa = present + (uint64_t)blockIdx.x * N;
+    pst = 1u;
+  }
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(axis, 0, 0x7fffffff, 0x00020000);
   // point p = 2r + h is shard p ^ M (rsmt2d order: data, then parity; Leopard order:
-  // parity, then data), at byte (p ^ M) * len = (2r ^ M) * len + h * len
-  const uint32_t vo = h * len + (active ? col : 0u);
+  // parity, then data), at byte (p ^ M) * sst = (2r ^ M) * sst + h * sst
+  const uint32_t vo = h * sst + (active ? col : 0u);
   uint32_t w[R];
 #pragma unroll
-  for (int r = 0; r < R; r++) w[r] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, (uint32_t)((2 * r) ^ M) * len, 2);
+  for (int r = 0; r < R; r++) w[r] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, (uint32_t)((2 * r) ^ M) * sst, 2);
 
   // error locator (the shard loads are in flight): err[i] = sum over erased e of
   // log(i ^ e) mod 255, an XOR convolution, by FWHT (as k_rs_decode)
-  const uint8_t* pa = present + (uint64_t)blockIdx.x * N;
   if (tid < N) {
-    const uint32_t pr = pa[tid ^ M] ? 1u : 0u;
+    const uint32_t pr = pa[(tid ^ M) * pst] ? 1u : 0u;
     s_pres[tid] = (uint8_t)pr;
     s_err[tid] = 1u - pr;
     s_tl[tid] = tid == 0 ? 0u : (uint32_t)c_t8.log[tid];
   }
   __syncthreads();
+  // in-square: the axis is complete once decoded (every presence read is above the barrier;
+  // the slice-0 workgroup of the axis marks it)
+  if (idx && blockIdx.y == 0 && tid < N) pa[tid * pst] = 1;
   auto fwht = [&](bool both) {
 #pragma unroll
     for (int lh = 0; lh < LOGN; lh++) {
@@ -287,7 +309,7 @@ __global__ __launch_bounds__(256, 2) void k_rs_decode_axis(uint8_t* __restrict__
   });
   // scale out and store the erased points: shard = work * exp(-err)
   if (!active) return;
-  uint32_t slen = len;  // recomputed shard offsets below (not 128 SGPRs live from the loads)
+  uint32_t slen = sst;  // recomputed shard offsets below (not 128 SGPRs live from the loads)
   asm volatile("" : "+s"(slen));
   uint32_t miss[NW];
   sfor<NW>([&](auto i) { miss[decltype(i)::value] = s_miss[h][decltype(i)::value]; });
@@ -300,11 +322,11 @@ __global__ __launch_bounds__(256, 2) void k_rs_decode_axis(uint8_t* __restrict__
 }
 
 template <int LOGN>
-hipError_t launch(uint8_t* shards, const uint8_t* present, uint32_t naxes, uint32_t len, const uint32_t* mul8,
-                  hipStream_t s) {
+hipError_t launch(uint8_t* shards, uint8_t* present, uint32_t naxes, uint32_t len, const uint32_t* mul8,
+                  const int32_t* idx, uint32_t W, int is_col, hipStream_t s) {
   const uint32_t nslice = (len + 127) / 128;
   hipLaunchKernelGGL(k_rs_decode_axis<LOGN>, dim3(naxes, (nslice + 3) / 4), dim3(256), 0, s, shards, present, len,
-                     mul8);
+                     mul8, idx, W, is_col);
   return hipGetLastError();
 }
 
@@ -314,17 +336,30 @@ bool rs_decode_axis_supported(uint32_t n, uint32_t len) {
   return n >= 32 && n <= 256 && (n & (n - 1)) == 0 && len > 0 && len % 64 == 0 && (uint64_t)n * len < 0x7fffffffull;
 }
 
+static hipError_t decode_axes(uint8_t* shards, uint8_t* present, uint32_t naxes, uint32_t n, uint32_t len,
+                              const uint32_t* mul8, const int32_t* idx, uint32_t W, int is_col, hipStream_t s) {
+  switch (n) {
+    case 32: return dx::launch<5>(shards, present, naxes, len, mul8, idx, W, is_col, s);
+    case 64: return dx::launch<6>(shards, present, naxes, len, mul8, idx, W, is_col, s);
+    case 128: return dx::launch<7>(shards, present, naxes, len, mul8, idx, W, is_col, s);
+    case 256: return dx::launch<8>(shards, present, naxes, len, mul8, idx, W, is_col, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 hipError_t launch_rs_decode_axis(uint8_t* shards, const uint8_t* present, uint32_t naxes, uint32_t n, uint32_t len,
                                  const uint32_t* mul8, hipStream_t s) {
   if (!rs_decode_axis_supported(n, len)) return hipErrorInvalidValue;
   if (naxes == 0) return hipSuccess;
-  switch (n) {
-    case 32: return dx::launch<5>(shards, present, naxes, len, mul8, s);
-    case 64: return dx::launch<6>(shards, present, naxes, len, mul8, s);
-    case 128: return dx::launch<7>(shards, present, naxes, len, mul8, s);
-    case 256: return dx::launch<8>(shards, present, naxes, len, mul8, s);
-    default: return hipErrorInvalidValue;
-  }
+  // dense mode never writes the presence bytes
+  return decode_axes(shards, const_cast<uint8_t*>(present), naxes, n, len, mul8, nullptr, 0, 0, s);
+}
+
+hipError_t launch_rs_decode_in_square(uint8_t* eds, uint8_t* mask, uint32_t W, const int32_t* idx, int is_col,
+                                      uint32_t naxes, const uint32_t* mul8, hipStream_t s) {
+  if (!rs_decode_axis_supported(W, kShare) || (uint64_t)W * W * kShare >= 0x7fffffffull) return hipErrorInvalidValue;
+  if (naxes == 0) return hipSuccess;
+  return decode_axes(eds, mask, naxes, W, kShare, mul8, idx, W, is_col, s);
 }
 
 }  // namespace cel
