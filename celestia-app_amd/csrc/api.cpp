@@ -1013,24 +1013,41 @@ struct MaskBits {
     }
     for (uint32_t i = 0; i < W; i++) total += cnt[0][i];
   }
-  // axis (is_col, i) gets all its cells; appends each orthogonal axis this completes to
-  // done, in ascending order
-  void fill(int is_col, uint32_t i, std::vector<int32_t>& done) {
-    uint64_t* a = bits[is_col].data() + (size_t)i * nw;
-    const uint64_t bit = 1ull << (i % 64);
-    for (uint32_t q = 0; q < nw; q++) {
-      const uint64_t valid = (q + 1) * 64 <= W ? ~0ull : ((1ull << (W % 64)) - 1);
-      uint64_t miss = ~a[q] & valid;
-      a[q] = valid;
-      while (miss) {
-        const uint32_t j = q * 64 + (uint32_t)__builtin_ctzll(miss);
-        miss &= miss - 1;
-        bits[!is_col][(size_t)j * nw + i / 64] |= bit;
-        total++;
-        if (++cnt[!is_col][j] == W) done.push_back((int32_t)j);
-      }
+  // A pass: every axis of `list` (direction is_col, ascending) gets all its cells.
+  // orth[t] = the orthogonal axes that solve list[t] completes, ascending: those whose
+  // missing cells all lie in listed axes, the last of them in list[t] (rsmt2d fills the
+  // axes one by one in list order). Word operations over the bitsets, O(W^2 / 64).
+  void fill_pass(int is_col, const std::vector<int32_t>& list, std::vector<std::vector<int32_t>>& orth) {
+    std::vector<uint64_t> S(nw, 0);
+    std::vector<int32_t> pos(W, -1);
+    for (size_t t = 0; t < list.size(); t++) {
+      S[(uint32_t)list[t] / 64] |= 1ull << ((uint32_t)list[t] % 64);
+      pos[list[t]] = (int32_t)t;
     }
-    cnt[is_col][i] = W;
+    orth.assign(list.size(), {});
+    for (uint32_t j = 0; j < W; j++) {
+      if (cnt[!is_col][j] == W) continue;
+      uint64_t* a = bits[!is_col].data() + (size_t)j * nw;
+      bool inside = true;
+      int32_t last = -1;
+      uint32_t c = 0;
+      for (uint32_t q = 0; q < nw; q++) {
+        const uint64_t valid = (q + 1) * 64 <= W ? ~0ull : ((1ull << (W % 64)) - 1);
+        const uint64_t miss = ~a[q] & valid;
+        if (miss & ~S[q]) inside = false;
+        if (miss) last = (int32_t)(q * 64 + 63 - __builtin_clzll(miss));
+        a[q] |= S[q];
+        c += (uint32_t)__builtin_popcountll(a[q] & valid);
+      }
+      total += c - cnt[!is_col][j];
+      cnt[!is_col][j] = c;
+      if (inside && last >= 0) orth[pos[last]].push_back((int32_t)j);
+    }
+    for (int32_t i : list) {
+      uint64_t* a = bits[is_col].data() + (size_t)i * nw;
+      for (uint32_t q = 0; q < nw; q++) a[q] = (q + 1) * 64 <= W ? ~0ull : ((1ull << (W % 64)) - 1);
+      cnt[is_col][i] = W;
+    }
   }
 };
 
@@ -1080,6 +1097,7 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
   }
   // solveCrossword: all rows, then all columns, until solved or stuck
   bool solved = false;
+  std::vector<std::vector<int32_t>> by_solve;
   for (;;) {
     bool progress = false;
     for (int is_col = 0; is_col < 2; is_col++) {
@@ -1096,14 +1114,16 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
         return st;
       }
       // sequential view of the pass: solve i fills its missing cells, completing the
-      // orthogonal axes whose only missing cell it was
-      for (int32_t i : list) {
+      // orthogonal axes whose last missing cell it held
+      mb.fill_pass(is_col, list, by_solve);
+      for (size_t t = 0; t < list.size(); t++) {
         const int32_t si = (int32_t)solves.size();
-        order.push_back({Check::SOLVE, is_col, i, si});
-        const size_t o0 = orth.size();
-        mb.fill(is_col, (uint32_t)i, orth);
-        for (size_t t = o0; t < orth.size(); t++) order.push_back({Check::ORTH, !is_col, orth[t], si});
-        solves.push_back({is_col, i});
+        order.push_back({Check::SOLVE, is_col, list[t], si});
+        for (int32_t j : by_solve[t]) {
+          order.push_back({Check::ORTH, !is_col, j, si});
+          orth.push_back(j);
+        }
+        solves.push_back({is_col, list[t]});
       }
       std::sort(orth.begin(), orth.end());
       if ((st = check_pass(ctx, b, k, !is_col, orth)) != CEL_OK) return st;
