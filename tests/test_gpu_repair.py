@@ -299,3 +299,59 @@ def test_orthogonal_completion_then_stuck(ctx, oracle):
                                            [x.tobytes() for x in cr])
     assert st == _lib.EBYZANTINE and bad == (1, c)
     assert bp.all() and np.array_equal(bs, eds[:, c])
+
+
+def _crossword_passes(present, k):
+    """Passes of rsmt2d's crossword loop over a presence mask alone (an axis with at least
+    k of its 2k cells gets all of them): (passes, solvable)."""
+    m = present.astype(bool).copy()
+    w, n = 2 * k, 0
+    while True:
+        progress = False
+        for ax in (0, 1):
+            cnt = m.sum(axis=1 - ax)
+            s = (cnt >= k) & (cnt < w)
+            if s.any():
+                if ax == 0:
+                    m[s, :] = True
+                else:
+                    m[:, s] = True
+                progress = True
+                n += 1
+        if m.all():
+            return n, True
+        if not progress:
+            return n, False
+
+
+@pytest.mark.parametrize("k,p,seed,npass,ok", [
+    (32, 0.40, 13, 9, True),     # register decoder in the square, nine alternating passes
+    (32, 0.40, 15, 3, False),    # stuck after three passes
+    (128, 0.44, 1, 5, True),
+    (256, 0.46, 2, 4, True),     # GF(2^16): gather -> LDS decoder -> scatter, both dense buffers
+    (256, 0.44, 25, 5, False),
+])
+def test_dev_repair_many_passes(ctx, oracle, k, p, seed, npass, ok):
+    """Masks whose crossword takes several row/column passes (the two-stream schedule:
+    solve chain on the main stream, encoding checks on the side stream, alternating dense
+    buffers for the LDS decoder): a solvable mask gives back the original EDS (the
+    codeword is unique), a stuck one EUNREPAIRABLE with every cell the final mask vouches
+    for equal to the original; k = 32 also against the oracle's restatement."""
+    from celestia_eds import _lib
+    eds, rr, cr = setup(oracle, k, seed=3)
+    w = 2 * k
+    present = (np.random.default_rng(seed).random((w, w)) < p).astype(np.uint8)
+    assert _crossword_passes(present, k) == (npass, ok)
+    st, cells, _, (_, _, after) = _dev_repair(ctx, eds, present, rr, cr, want_shares=True)
+    if ok:
+        assert st == _lib.OK and np.array_equal(cells, eds)
+    else:
+        assert st == _lib.EUNREPAIRABLE
+        assert np.array_equal(cells[after == 1], eds[after == 1])
+        assert (after >= present).all() and after.sum() > present.sum()
+    if k == 32:
+        damaged = eds.copy()
+        damaged[present == 0] = 0
+        rc, ocells, opres, _ = oracle.repair(damaged, present, _stack(rr), _stack(cr))
+        assert rc == st
+        assert np.array_equal(after, opres)
