@@ -450,7 +450,8 @@ def _measure_batch(ctx, local, rank, k, B, steps, warmup, n_distinct, layout, ph
 def measure_host_io(ctx, k, n=16, reps=3):
     """cel_extend_batch over page-locked host buffers (cel_host_alloc): n ODSs in, then
     (a) the EDS + roots + DAH out (what rsmt2d.ImportExtendedDataSquare needs) and
-    (b) roots + DAH only (PrepareProposal/ProcessProposal keep only the DAH,
+    (b) the parity cells only (CEL_FLAG_PARITY_ONLY: the caller holds Q0 already) and
+    (c) roots + DAH only (PrepareProposal/ProcessProposal keep only the DAH,
     app/prepare_proposal.go:81-83). PCIe copies included; never the headline value."""
     import ctypes
     from celestia_eds import _lib
@@ -473,16 +474,18 @@ def measure_host_io(ctx, k, n=16, reps=3):
     P = lambda x: x.ctypes.data_as(ctypes.c_void_p)
     out = {}
     try:
-        for name, e in (("with_eds", eds), ("roots_only", None)):
+        for name, e, fl in (("with_eds", eds, 0), ("parity_only", eds, _lib.FLAG_PARITY_ONLY),
+                            ("roots_only", None, 0)):
             def once():
                 ctx.check(ctx.lib.cel_extend_batch(ctx.handle, P(ods), n, k, 512, P(e) if e is not None else None,
-                                                   P(rr), P(cr), P(dah), P(st), _lib.FLAG_ORDER_CHECK))
+                                                   P(rr), P(cr), P(dah), P(st), _lib.FLAG_ORDER_CHECK | fl))
             once()
             t0 = time.perf_counter()
             for _ in range(reps):
                 once()
             dt = (time.perf_counter() - t0) / reps
-            pcie = ods.nbytes + (eds.nbytes if e is not None else 0) + rr.nbytes + cr.nbytes
+            eds_b = 0 if e is None else (eds.nbytes * 3 // 4 if fl else eds.nbytes)
+            pcie = ods.nbytes + eds_b + rr.nbytes + cr.nbytes
             out[name] = {"squares_per_s": n / dt, "pcie_gbps": pcie / dt / 1e9, "ms_per_call": dt * 1e3}
     finally:
         ctx.lib.cel_host_free(p_ods)

@@ -16,6 +16,7 @@ LIB_PATH = os.environ.get("CEL_EDS_LIB", os.path.join(_ROOT, "libcelestia_eds.so
 OK, EINVAL, ENOTPOW2, ECHUNK, ETOOBIG, EORDER, ETOOFEW, EBYZANTINE, EUNREPAIRABLE, EDEVICE, ENOMEM, \
     ESHORT, EPUSHPAST, EBADROOT = range(14)
 FLAG_ORDER_CHECK = 0x1
+FLAG_PARITY_ONLY = 0x2
 SHARE_SIZE = 512
 NAMESPACE_SIZE = 29
 NMT_NODE_SIZE = 90

@@ -336,9 +336,23 @@ cel_status cel_extend_batch(cel_ctx* ctx, const uint8_t* ods, uint32_t n, uint32
     const uint32_t first = c * chunk, cnt = (first + chunk <= n) ? chunk : n - first;
     hipStream_t cs = ctx->sub[c % cel_ctx::kPipe];
     uint8_t* eds_c = d_eds + first * eds_sq;
-    if ((eds_out && (e = hipMemcpyAsync(eds_out + first * eds_sq, eds_c, cnt * eds_sq, hipMemcpyDeviceToHost, cs)) !=
-                        hipSuccess) ||
-        (e = hipMemcpyAsync(row_roots + first * roots_sq, d_rr + first * roots_sq, cnt * roots_sq,
+    if (eds_out && (flags & CEL_FLAG_PARITY_ONLY)) {
+      // Q1 (the right half of rows 0..k-1, one strided copy) then Q2|Q3 (contiguous)
+      const size_t half = (size_t)k * kShare;
+      for (uint32_t i = 0; i < cnt && e == hipSuccess; i++) {
+        uint8_t* h = eds_out + (first + i) * eds_sq;
+        const uint8_t* d = eds_c + i * eds_sq;
+        if ((e = hipMemcpy2DAsync(h + half, 2 * half, d + half, 2 * half, half, k, hipMemcpyDeviceToHost, cs)) ==
+            hipSuccess)
+          e = hipMemcpyAsync(h + eds_sq / 2, d + eds_sq / 2, eds_sq / 2, hipMemcpyDeviceToHost, cs);
+      }
+      if (e != hipSuccess) return hip_fail(ctx, e, "D2H");
+    } else if (eds_out &&
+               (e = hipMemcpyAsync(eds_out + first * eds_sq, eds_c, cnt * eds_sq, hipMemcpyDeviceToHost, cs)) !=
+                   hipSuccess) {
+      return hip_fail(ctx, e, "D2H");
+    }
+    if ((e = hipMemcpyAsync(row_roots + first * roots_sq, d_rr + first * roots_sq, cnt * roots_sq,
                             hipMemcpyDeviceToHost, cs)) != hipSuccess ||
         (e = hipMemcpyAsync(col_roots + first * roots_sq, d_cr + first * roots_sq, cnt * roots_sq,
                             hipMemcpyDeviceToHost, cs)) != hipSuccess ||

@@ -34,6 +34,7 @@ const (
 	ShareSize    = C.CEL_SHARE_SIZE
 	NmtNodeSize  = C.CEL_NMT_NODE_SIZE
 	flagOrder    = C.CEL_FLAG_ORDER_CHECK
+	flagParity   = C.CEL_FLAG_PARITY_ONLY
 )
 
 // Status codes map onto the reference's Go errors (include/celestia_eds.h):
@@ -84,6 +85,8 @@ func (c *Context) errLocked(st C.cel_status) error {
 // the flattened EDS plus all 4k roots and the DAH hash come back in one call.
 // The caller wraps the result with rsmt2d.ImportExtendedDataSquare(flat, codec,
 // RootTableConstructor(rowRoots, colRoots)) so NewDataAvailabilityHeader is unchanged.
+// Only the parity cells cross PCIe (CEL_FLAG_PARITY_ONLY): flat's Q0 cells are left
+// zero, ExtendSquare points them at the input shares.
 func (c *Context) ExtendShares(shares [][]byte) (flat []byte, rowRoots, colRoots [][]byte, dah []byte, err error) {
 	n := len(shares)
 	buf := C.malloc(C.size_t(n * ShareSize))
@@ -104,7 +107,7 @@ func (c *Context) ExtendShares(shares [][]byte) (flat []byte, rowRoots, colRoots
 	err = c.call(func() C.cel_status {
 		return C.cel_extend_shares(c.ctx, (*C.uint8_t)(buf), C.uint32_t(n), ShareSize,
 			(*C.uint8_t)(unsafe.Pointer(&flat[0])), (*C.uint8_t)(unsafe.Pointer(&rr[0])),
-			(*C.uint8_t)(unsafe.Pointer(&cr[0])), (*C.uint8_t)(unsafe.Pointer(&dah[0])), flagOrder)
+			(*C.uint8_t)(unsafe.Pointer(&cr[0])), (*C.uint8_t)(unsafe.Pointer(&dah[0])), flagOrder|flagParity)
 	})
 	if err != nil {
 		return nil, nil, nil, nil, err
@@ -129,9 +132,14 @@ func (c *Context) ExtendSquare(shares [][]byte, codec rsmt2d.Codec) (*rsmt2d.Ext
 		return nil, err
 	}
 	w := len(rr)
+	k := w / 2
 	cells := make([][]byte, w*w)
 	for i := range cells {
-		cells[i] = flat[i*ShareSize : (i+1)*ShareSize]
+		if r, col := i/w, i%w; r < k && col < k {
+			cells[i] = shares[r*k+col] // Q0: the ODS itself (not copied back)
+		} else {
+			cells[i] = flat[i*ShareSize : (i+1)*ShareSize]
+		}
 	}
 	table := &RootTable{Rows: rr, Cols: cr, Cells: cells, Width: w}
 	return rsmt2d.ImportExtendedDataSquare(cells, codec, table.NewTree)

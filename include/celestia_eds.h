@@ -54,6 +54,10 @@ typedef int32_t cel_status;
 
 /* Flags for the square entry points. */
 #define CEL_FLAG_ORDER_CHECK 0x1u   /* enforce the honest nmt push order (default in the Go path) */
+#define CEL_FLAG_PARITY_ONLY 0x2u   /* host entry points: eds_out receives the parity cells only
+                                       (Q1, Q2, Q3); its Q0 cells are not written, the caller
+                                       holds the ODS already (the Go shim points Q0's cells of the
+                                       imported square at the input shares): 3/4 of the PCIe bytes */
 
 #define CEL_SHARE_SIZE 512u
 #define CEL_NAMESPACE_SIZE 29u

@@ -288,3 +288,26 @@ def test_dah_hash_any_root_length(ctx):
         w = len(rows)
         want = rfc(rows + (cols[:w] + [b""] * max(0, w - len(cols))))
         assert da.DataAvailabilityHeader(rows, cols).Hash() == want, (len(rows), len(cols))
+
+
+@pytest.mark.parametrize("k,n", [(16, 3), (128, 5)])
+def test_batch_parity_only(ctx, oracle, k, n):
+    """CEL_FLAG_PARITY_ONLY: the host path copies back Q1, Q2, Q3 only (Q1 as one strided
+    copy per square); the caller's Q0 bytes stay untouched, every parity cell, root and
+    DAH equals the oracle's."""
+    import ctypes
+    from celestia_eds import _lib
+    odss = np.stack([random_ods(k, 300 + 5 * i + k) for i in range(n)])
+    rr = np.zeros((n, 2 * k, 90), np.uint8)
+    cr = np.zeros_like(rr)
+    dah = np.zeros((n, 32), np.uint8)
+    eds = np.full((n, 2 * k, 2 * k, 512), 0xA5, np.uint8)
+    st = np.zeros(n, np.int32)
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    ctx.check(ctx.lib.cel_extend_batch(ctx.handle, P(odss), n, k, 512, P(eds), P(rr), P(cr), P(dah), P(st),
+                                       _lib.FLAG_ORDER_CHECK | _lib.FLAG_PARITY_ONLY))
+    for i in range(n):
+        e, r, c, d = oracle.extend_and_commit(odss[i])
+        assert (eds[i, :k, :k] == 0xA5).all(), f"square {i}: Q0 was written"
+        assert np.array_equal(eds[i, :k, k:], e[:k, k:]) and np.array_equal(eds[i, k:], e[k:]), f"square {i}: parity"
+        assert np.array_equal(rr[i], r) and np.array_equal(cr[i], c) and dah[i].tobytes() == d
