@@ -487,6 +487,16 @@ def measure_host_io(ctx, k, n=16, reps=3):
             eds_b = 0 if e is None else (eds.nbytes * 3 // 4 if fl else eds.nbytes)
             pcie = ods.nbytes + eds_b + rr.nbytes + cr.nbytes
             out[name] = {"squares_per_s": n / dt, "pcie_gbps": pcie / dt / 1e9, "ms_per_call": dt * 1e3}
+        # one square per call: da.ExtendShares as PrepareProposal / ProcessProposal issue it
+        # (one block, one square), parity cells back
+        def one():
+            ctx.check(ctx.lib.cel_extend_batch(ctx.handle, P(ods), 1, k, 512, P(eds), P(rr), P(cr), P(dah), P(st),
+                                               _lib.FLAG_ORDER_CHECK | _lib.FLAG_PARITY_ONLY))
+        one()
+        t0 = time.perf_counter()
+        for _ in range(10):
+            one()
+        out["single_square_parity_only_ms"] = (time.perf_counter() - t0) / 10 * 1e3
     finally:
         ctx.lib.cel_host_free(p_ods)
         ctx.lib.cel_host_free(p_eds)

@@ -99,6 +99,10 @@ cel_status cel_ctx_create(int device, cel_ctx** out) {
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_rs[i], hipEventDisableTiming);
   }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_start, hipEventDisableTiming);
+  for (int i = 0; i < cel_ctx::kPipe && e == hipSuccess; i++) {
+    e = hipEventCreateWithFlags(&ctx->ev_dl[i], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->dl[i], hipStreamNonBlocking);
+  }
   if (e == hipSuccess) e = upload_tables(&ctx->tables);
   if (e != hipSuccess) {
     cel_ctx_destroy(ctx);
@@ -124,6 +128,13 @@ void cel_ctx_destroy(cel_ctx* ctx) {
       if (ctx->ev_rs[i]) (void)hipEventDestroy(ctx->ev_rs[i]);
     }
     if (ctx->ev_start) (void)hipEventDestroy(ctx->ev_start);
+    for (int i = 0; i < cel_ctx::kPipe; i++) {
+      if (ctx->dl[i]) {
+        (void)hipStreamSynchronize(ctx->dl[i]);
+        (void)hipStreamDestroy(ctx->dl[i]);
+      }
+      if (ctx->ev_dl[i]) (void)hipEventDestroy(ctx->ev_dl[i]);
+    }
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   }
   delete ctx;
@@ -325,31 +336,35 @@ cel_status cel_extend_batch(cel_ctx* ctx, const uint8_t* ods, uint32_t n, uint32
     if ((e = hipStreamWaitEvent(cs, ctx->ev_start, 0)) != hipSuccess ||
         (e = place_ods(ods + first * ods_sq, cnt, k, eds_c, cs)) != hipSuccess ||
         (e = launch_extend(nullptr, eds_c, k, cnt, ctx->tables, cs)) != hipSuccess ||
+        (e = hipEventRecord(ctx->ev_rs[c % cel_ctx::kChunks], cs)) != hipSuccess ||
         (e = launch_commit(eds_c, k, cnt, d_rr + first * roots_sq, d_cr + first * roots_sq, d_dah + first * 32,
                            d_st + first, d_work + (c % cel_ctx::kPipe) * ws, (flags & CEL_FLAG_ORDER_CHECK) != 0,
                            cs)) != hipSuccess)
       return hip_fail(ctx, e, "extend batch");
   }
   // Downloads after every chunk is enqueued: a copy into pageable memory blocks the
-  // calling thread, and the later chunks' kernels run meanwhile.
+  // calling thread, and the later chunks' kernels run meanwhile. A chunk's EDS goes back
+  // on the download stream as soon as its extension is done, beside its own hashing.
   for (uint32_t c = 0; c < nchunks; c++) {
     const uint32_t first = c * chunk, cnt = (first + chunk <= n) ? chunk : n - first;
     hipStream_t cs = ctx->sub[c % cel_ctx::kPipe];
     uint8_t* eds_c = d_eds + first * eds_sq;
+    hipStream_t ds = ctx->dl[c % cel_ctx::kPipe];
+    if (eds_out && (e = hipStreamWaitEvent(ds, ctx->ev_rs[c % cel_ctx::kChunks], 0)) != hipSuccess)
+      return hip_fail(ctx, e, "event");
     if (eds_out && (flags & CEL_FLAG_PARITY_ONLY)) {
       // Q1 (the right half of rows 0..k-1, one strided copy) then Q2|Q3 (contiguous)
       const size_t half = (size_t)k * kShare;
       for (uint32_t i = 0; i < cnt && e == hipSuccess; i++) {
         uint8_t* h = eds_out + (first + i) * eds_sq;
         const uint8_t* d = eds_c + i * eds_sq;
-        if ((e = hipMemcpy2DAsync(h + half, 2 * half, d + half, 2 * half, half, k, hipMemcpyDeviceToHost, cs)) ==
+        if ((e = hipMemcpy2DAsync(h + half, 2 * half, d + half, 2 * half, half, k, hipMemcpyDeviceToHost, ds)) ==
             hipSuccess)
-          e = hipMemcpyAsync(h + eds_sq / 2, d + eds_sq / 2, eds_sq / 2, hipMemcpyDeviceToHost, cs);
+          e = hipMemcpyAsync(h + eds_sq / 2, d + eds_sq / 2, eds_sq / 2, hipMemcpyDeviceToHost, ds);
       }
       if (e != hipSuccess) return hip_fail(ctx, e, "D2H");
-    } else if (eds_out &&
-               (e = hipMemcpyAsync(eds_out + first * eds_sq, eds_c, cnt * eds_sq, hipMemcpyDeviceToHost, cs)) !=
-                   hipSuccess) {
+    } else if (eds_out && (e = hipMemcpyAsync(eds_out + first * eds_sq, eds_c, cnt * eds_sq, hipMemcpyDeviceToHost,
+                                              ds)) != hipSuccess) {
       return hip_fail(ctx, e, "D2H");
     }
     if ((e = hipMemcpyAsync(row_roots + first * roots_sq, d_rr + first * roots_sq, cnt * roots_sq,
@@ -365,6 +380,10 @@ cel_status cel_extend_batch(cel_ctx* ctx, const uint8_t* ods, uint32_t n, uint32
         (e = hipStreamWaitEvent(s, ctx->ev_done[c % cel_ctx::kChunks], 0)) != hipSuccess)
       return hip_fail(ctx, e, "event");
   }
+  for (uint32_t i = 0; eds_out && i < nstreams; i++)
+    if ((e = hipEventRecord(ctx->ev_dl[i], ctx->dl[i])) != hipSuccess ||
+        (e = hipStreamWaitEvent(s, ctx->ev_dl[i], 0)) != hipSuccess)
+      return hip_fail(ctx, e, "event");
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "sync");
   cel_status worst = CEL_OK;
   for (uint32_t i = 0; i < n; i++) {

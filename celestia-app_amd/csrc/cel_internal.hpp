@@ -170,6 +170,9 @@ struct cel_ctx {
   hipEvent_t ev_start = nullptr;
   hipEvent_t ev_done[kChunks] = {};
   hipEvent_t ev_rs[kChunks] = {};
+  // EDS downloads of the host pipeline, one per pipeline stream (beside the hashing)
+  hipStream_t dl[kPipe] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev_dl[kPipe] = {};
   std::mutex mu;
   cel::DeviceTables tables;
   std::string last_error;
