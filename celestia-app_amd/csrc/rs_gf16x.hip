@@ -390,7 +390,7 @@ __global__ __launch_bounds__(256, LOGK == 9 ? 3 : 4) void k_rs_gf16x(RsGeom g) {
 #pragma unroll
     for (int i = 0; i < NR; i++) {
       const uint32_t so = __builtin_amdgcn_readfirstlane(reg_bits((uint32_t)i) * in_shard);
-      const auto v = __builtin_amdgcn_raw_buffer_load_b64(rin, vin, so, 2);
+      const auto v = __builtin_amdgcn_raw_buffer_load_b64(rin, vin, so, 0);
       w[2 * i] = v[0];
       w[2 * i + 1] = v[1];
     }
@@ -437,7 +437,7 @@ __global__ __launch_bounds__(256, LOGK == 9 ? 3 : 4) void k_rs_gf16x(RsGeom g) {
 #pragma unroll
   for (int i = 0; i < NR; i++) {
     const uint32_t so = __builtin_amdgcn_readfirstlane(place(reg_bits((uint32_t)i), out_shard, out_blk));
-    __builtin_amdgcn_raw_buffer_store_b64(D2{w[2 * i], w[2 * i + 1]}, rout, vout, so, 2);
+    __builtin_amdgcn_raw_buffer_store_b64(D2{w[2 * i], w[2 * i + 1]}, rout, vout, so, 0);
   }
 }
 
