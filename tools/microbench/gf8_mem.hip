@@ -39,7 +39,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
 }
 
-template <int MAP, int F>
+template <int MAP, int F, int POL = 2>
 __global__ __launch_bounds__(256, 3) void k_mem(Geo g) {
   constexpr int K = 128;
   const uint32_t lane = threadIdx.x & 63;
@@ -51,7 +51,7 @@ __global__ __launch_bounds__(256, 3) void k_mem(Geo g) {
   uint32_t w[K];
   if constexpr (MAP == 0) {
 #pragma unroll
-    for (int i = 0; i < K; i++) w[i] = __builtin_amdgcn_raw_buffer_load_b32(rin, lane * 4u, i * g.in_shard, 2);
+    for (int i = 0; i < K; i++) w[i] = __builtin_amdgcn_raw_buffer_load_b32(rin, lane * 4u, i * g.in_shard, POL);
   } else if constexpr (MAP == 1) {
     const uint32_t s = lane >> 5, o = (lane & 31u) * 8u;
 #pragma unroll
@@ -78,7 +78,7 @@ __global__ __launch_bounds__(256, 3) void k_mem(Geo g) {
   }
   if constexpr (MAP == 0) {
 #pragma unroll
-    for (int i = 0; i < K; i++) __builtin_amdgcn_raw_buffer_store_b32(w[i], rout, lane * 4u, i * g.out_shard, 2);
+    for (int i = 0; i < K; i++) __builtin_amdgcn_raw_buffer_store_b32(w[i], rout, lane * 4u, i * g.out_shard, POL);
   } else if constexpr (MAP == 1) {
     const uint32_t s = lane >> 5, o = (lane & 31u) * 8u;
 #pragma unroll
@@ -94,6 +94,32 @@ __global__ __launch_bounds__(256, 3) void k_mem(Geo g) {
       __builtin_amdgcn_raw_buffer_store_b128(v, rout, s * g.out_shard + o, 4 * i * g.out_shard, 2);
     }
   }
+}
+
+// rows then columns of C squares at a time (the Infinity-Cache schedule: a chunk's [Q0|Q1]
+// is re-read by its column pass while it may still sit in the 256 MB MALL)
+template <int POL>
+static float run_chunked(Geo rows, Geo cols, uint32_t C, int reps) {
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  auto once = [&]() {
+    for (uint32_t z = 0; z < rows.nsq; z += C) {
+      Geo r = rows, c = cols;
+      r.in += z * rows.sq; r.out += z * rows.sq; r.nsq = C;
+      c.in += z * cols.sq; c.out += z * cols.sq; c.nsq = C;
+      hipLaunchKernelGGL((k_mem<0, 0, POL>), dim3((r.axes * 2u * C + 3) / 4), dim3(256), 0, 0, r);
+      hipLaunchKernelGGL((k_mem<0, 0, POL>), dim3((c.axes * 2u * C + 3) / 4), dim3(256), 0, 0, c);
+    }
+  };
+  once();
+  CK(hipEventRecord(a));
+  for (int i = 0; i < reps; i++) once();
+  CK(hipEventRecord(b));
+  CK(hipEventSynchronize(b));
+  float ms;
+  CK(hipEventElapsedTime(&ms, a, b));
+  return ms / reps;
 }
 
 template <int MAP, int F>
@@ -136,6 +162,13 @@ int main() {
   rep("rows map2 F=8", run<2, 8>(rows, 10), rb);
   rep("cols map0 F=8", run<0, 8>(cols, 10), cb);
   rep("cols map2 F=8", run<2, 8>(cols, 10), cb);
+  for (uint32_t C : {64u, 16u, 8u, 4u, 2u}) {
+    char n1[64], n2[64];
+    snprintf(n1, sizeof n1, "pair chunk %u nt", C);
+    snprintf(n2, sizeof n2, "pair chunk %u default", C);
+    rep(n1, run_chunked<2>(rows, cols, C, 5), rb + cb);
+    rep(n2, run_chunked<0>(rows, cols, C, 5), rb + cb);
+  }
   CK(hipFree(eds));
   return 0;
 }
