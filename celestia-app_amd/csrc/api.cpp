@@ -1097,6 +1097,11 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
   hipStream_t s = b.main;
   hipError_t e = hipSuccess;
   cel_status st;
+  // an early return leaves no side-stream work running on the ctx's scratch buffers
+  struct SideDrain {
+    hipStream_t side;
+    ~SideDrain() { (void)hipStreamSynchronize(side); }
+  } drain{b.side};
   std::memcpy(b.hmask, hm.data(), cells);
   if ((e = hipMemcpyAsync(b.mask, b.hmask, cells, hipMemcpyHostToDevice, s)) != hipSuccess ||
       (e = hipMemsetAsync(b.flags, 0, 2 * (size_t)W * 4, s)) != hipSuccess ||
