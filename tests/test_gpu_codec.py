@@ -24,7 +24,8 @@ def test_model_digest(ctx, golden, k):
         assert hashlib.sha256(got).hexdigest() == golden["leopard_model"][str(k)]["parity_sha256"]
 
 
-@pytest.mark.parametrize("n,ln", [(1, 64), (4, 64), (8, 192), (64, 512), (128, 512), (256, 128), (1024, 64)])
+@pytest.mark.parametrize("n,ln", [(1, 64), (4, 64), (8, 192), (64, 512), (128, 512), (256, 128), (256, 512), (512, 512),
+                                  (512, 1024), (1024, 64)])
 def test_encode_matches_oracle(ctx, oracle, n, ln):
     from celestia_eds.rsmt2d import LeoRSCodec
     rng = np.random.default_rng(n * 7 + ln)
