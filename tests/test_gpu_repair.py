@@ -355,3 +355,23 @@ def test_dev_repair_many_passes(ctx, oracle, k, p, seed, npass, ok):
         rc, ocells, opres, _ = oracle.repair(damaged, present, _stack(rr), _stack(cr))
         assert rc == st
         assert np.array_equal(after, opres)
+
+
+@pytest.mark.parametrize("k", [128, 256])
+def test_dev_repair_random_masks(ctx, oracle, k):
+    """18 random masks near the repair threshold (2-5 crossword passes): every outcome as
+    the mask's crossword predicts (solvable -> OK and the original EDS, stuck ->
+    EUNREPAIRABLE), through the two-stream schedule (k=128: in-square register decoder,
+    k=256: gather -> LDS decoder -> scatter with alternating dense buffers)."""
+    from celestia_eds import _lib
+    eds, rr, cr = setup(oracle, k, seed=3)
+    w = 2 * k
+    for seed in range(6):
+        for p in (0.44, 0.46, 0.5):
+            present = (np.random.default_rng(seed).random((w, w)) < p).astype(np.uint8)
+            _, ok = _crossword_passes(present, k)
+            st, cells, _ = _dev_repair(ctx, eds, present, rr, cr)
+            if ok:
+                assert st == _lib.OK and np.array_equal(cells, eds), (seed, p)
+            else:
+                assert st == _lib.EUNREPAIRABLE, (seed, p, st)
