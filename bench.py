@@ -13,7 +13,8 @@ Besides the headline number the JSON line carries:
   roofline      RS extension (both passes) vs HBM: algorithmic 2048 k^2 bytes per
                 square / measured average duration (HIP events on the launch stream)
   roofline_nmt  NMT+DAH phase: SHA-256 compressions (60 k^2 + 4k - 2 per square)
-                per second vs the integer-VALU issue peak
+                per second vs the measured SHA-256 peak of the same compression code with
+                no memory traffic (and, as peak_model, the op-rate model of its mix)
   k512          (default --k 128 run) the same measurement on a short batch of k=512
                 squares (GF(2^16)), since the metric names k=128 and k=512
   cpu_baseline  the C restatement (oracle/, SIMD + OpenMP) on a bounded sample of the
@@ -43,6 +44,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table)
 # measured per-op rates of profiles/r1_microbench_valu.txt is ~4.5k cycles per compression
 # per wave: 1024 SIMDs x 2.4 GHz x 64 / 4528 = 34.7 G compressions/s.
 SHA_MIX_CEILING = 1024 * 2.4e9 * 64 / 4528
+# Measured SHA-256 peak: the NMT kernels' compression (cel::sha256_compress) chained in
+# registers on every lane, no memory traffic, 4-32 waves per SIMD: 29.1-29.6 G
+# compressions/s on two boxes (tools/microbench/sha_rate.hip, profiles/r2_sha_rate.txt).
+SHA_MEASURED_PEAK = 29.4e9
 # Measured HBM traffic of the RS extension (rocprofv3 FETCH_SIZE/WRITE_SIZE passes).
 # (input layout -> profile): ODS in Q0 of the EDS (in place) / separate ODS buffer.
 TRAFFIC_PROFILE = {"eds": "r1e_rs_traffic_inplace.json", "ods": "r1_rs_traffic.json"}
@@ -584,9 +589,12 @@ def main():
             "kernel": "nmt_commit (k_leaf + k_level x log2(2k) + k_merkle)",
             "achieved": nmt_rate / 1e9,
             "unit": "G SHA-256 compressions/s",
-            "peak": SHA_MIX_CEILING / 1e9,
-            "peak_basis": "SHA-256 instruction mix at measured per-op VALU rates (profiles/r1_microbench_valu.txt)",
-            "frac": nmt_rate / SHA_MIX_CEILING,
+            "peak": SHA_MEASURED_PEAK / 1e9,
+            "peak_basis": "measured SHA-256 compression rate with no memory traffic (profiles/r2_sha_rate.txt)",
+            "frac": nmt_rate / SHA_MEASURED_PEAK,
+            "peak_model": SHA_MIX_CEILING / 1e9,
+            "frac_model": nmt_rate / SHA_MIX_CEILING,
+            "peak_model_basis": "SHA-256 instruction mix at measured per-op VALU rates (profiles/r1_microbench_valu.txt)",
             "avg_launch_us": t_com * 1e6,
         },
     }
@@ -609,7 +617,8 @@ def main():
             "squares_per_step_per_gpu": B5, "steps": a.k512_steps,
             "ms_per_step": t5 / a.k512_steps * 1e3,
             "rs_frac_hbm": rs5 / HBM_PEAK_GBS, "rs_avg_launch_us": m5["t_ext"] * 1e6,
-            "nmt_frac_sha_mix": comp5 / SHA_MIX_CEILING, "nmt_avg_launch_us": m5["t_com"] * 1e6,
+            "nmt_frac_sha_peak": comp5 / SHA_MEASURED_PEAK, "nmt_frac_sha_mix": comp5 / SHA_MIX_CEILING,
+            "nmt_avg_launch_us": m5["t_com"] * 1e6,
         }
         del m5
         torch.cuda.empty_cache()
