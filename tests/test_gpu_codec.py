@@ -25,7 +25,7 @@ def test_model_digest(ctx, golden, k):
 
 
 @pytest.mark.parametrize("n,ln", [(1, 64), (4, 64), (8, 192), (64, 512), (128, 512), (256, 128), (256, 512), (512, 512),
-                                  (512, 1024), (1024, 64)])
+                                  (512, 1024), (1024, 64), (2048, 64)])
 def test_encode_matches_oracle(ctx, oracle, n, ln):
     from celestia_eds.rsmt2d import LeoRSCodec
     rng = np.random.default_rng(n * 7 + ln)
@@ -34,7 +34,7 @@ def test_encode_matches_oracle(ctx, oracle, n, ln):
     assert np.array_equal(np.frombuffer(b"".join(par), np.uint8).reshape(n, ln), oracle.rs_encode(data))
 
 
-@pytest.mark.parametrize("n", [1, 2, 8, 64, 128, 256, 512])
+@pytest.mark.parametrize("n", [1, 2, 8, 64, 128, 256, 512, 1024])
 def test_decode_random_erasures(ctx, oracle, n):
     from celestia_eds.rsmt2d import LeoRSCodec
     codec = LeoRSCodec(ctx)
@@ -70,3 +70,17 @@ def test_decode_too_few(ctx):
     with pytest.raises(CelError) as ei:
         LeoRSCodec(ctx).Decode(shards)
     assert ei.value.status == _lib.ETOOFEW
+
+
+def test_device_limits(ctx):
+    """The device codec's shard-count limits fail loudly (ETOOBIG), never fall back:
+    encode takes n <= 2048 data shards (the LDS image), decode n <= 1024."""
+    from celestia_eds import CelError, _lib
+    from celestia_eds.rsmt2d import LeoRSCodec
+    codec = LeoRSCodec(ctx)
+    with pytest.raises(CelError) as ei:
+        codec.Encode([bytes(64)] * 4096)
+    assert ei.value.status == _lib.ETOOBIG
+    with pytest.raises(CelError) as ei:
+        codec.Decode([bytes(64)] * 2048 + [None] * 2048)
+    assert ei.value.status == _lib.ETOOBIG
