@@ -268,7 +268,7 @@ def run_sharded(a):
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_rs_encode_gf16p (row pass of this rank)",
+            "kernel": "k_rs_gf16x (row pass of this rank, blocked all-to-all layout)",
             "achieved": rows_bytes / t_rows / 1e9,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
