@@ -112,8 +112,10 @@ class ShardedSquare:
         S, W = _lib.SHARE_SIZE, 2 * k
         e = steps.empty
         self.ods_rows = e((self.rows_per_rank, k, S), u8)
-        self.send = e((n, self.rows_per_rank, self.w, S), u8)
         self.slab = e((W, self.w, S), u8)
+        # one rank: the all-to-all is the identity, so the row pass writes the slab's top
+        # half directly (no 2k x k-cell copy)
+        self.send = self.slab[:k].view(1, k, W, S) if n == 1 else e((n, self.rows_per_rank, self.w, S), u8)
         self.col_rec = e((self.w, RECORD), u8)
         self.row_sub = e((W, RECORD), u8)
         self.row_sub_all = e((n, W, RECORD), u8)
@@ -131,6 +133,8 @@ class ShardedSquare:
         self.steps.rows(self.ods_rows, self.k, self.n, self.send)
 
     def exchange(self, comm):
+        if self.n == 1:  # send aliases the slab's top half
+            return
         top = self.slab[: self.k].view(self.n, self.rows_per_rank, self.w, _lib.SHARE_SIZE)
         comm.all_to_all(top.view(-1), self.send.view(-1))
 
@@ -184,7 +188,8 @@ class LocalComm:
         for h, dst in enumerate(squares):  # block h of every sender -> receiver h, sender order
             top = dst.slab[: dst.k].view(n, dst.rows_per_rank, dst.w, _lib.SHARE_SIZE)
             for r, src in enumerate(squares):
-                top[r].copy_(src.send[h])
+                if top[r].data_ptr() != src.send[h].data_ptr():  # aliased at n = 1
+                    top[r].copy_(src.send[h])
         for s in squares:
             s.phase_cols()
         row_sub_all = torch.stack([s.row_sub for s in squares])

@@ -52,7 +52,7 @@ class OracleSteps:
         for j in range(w):
             rc, root = oracle.axis_root(np.ascontiguousarray(s[:, j]), k, c0 + j, self.order_check)
             bad |= rc != 0
-            col_rec[j] = torch.from_numpy(record(root))
+            col_rec[j] = torch.from_numpy(record(root).copy())
         for i in range(2 * k):
             leaves = []
             for j in range(w):
@@ -61,7 +61,7 @@ class OracleSteps:
                 leaves.append(ns + cell)
             rc, root = oracle.nmt_root(leaves, self.order_check)
             bad |= rc != 0
-            row_sub[i] = torch.from_numpy(record(root))
+            row_sub[i] = torch.from_numpy(record(root).copy())
         status[0] = EORDER if bad else 0
 
     def finish(self, row_sub_all, col_rec_all, k, n, row_roots, col_roots, dah, status):
@@ -76,8 +76,8 @@ class OracleSteps:
                         bad = True
             while len(nodes) > 1:
                 nodes = [hash_node(nodes[2 * j], nodes[2 * j + 1]) for j in range(len(nodes) // 2)]
-            row_roots[i] = torch.from_numpy(np.frombuffer(nodes[0], np.uint8))
+            row_roots[i] = torch.from_numpy(np.frombuffer(nodes[0], np.uint8).copy())
         col_roots.copy_(col_rec_all[:, :90])
-        dah.copy_(torch.from_numpy(np.frombuffer(oracle.dah_hash(row_roots.numpy(), col_roots.numpy()), np.uint8)))
+        dah.copy_(torch.from_numpy(np.frombuffer(oracle.dah_hash(row_roots.numpy(), col_roots.numpy()), np.uint8).copy()))
         if bad:
             status[0] = EORDER

@@ -79,6 +79,37 @@ def test_gloo_sharded_order_violation(oracle):
     assert all(st == 5 for _, _, _, _, st in res)
 
 
+@pytest.mark.parametrize("local", [True, False])
+def test_one_rank_aliases_slab(oracle, local):
+    """One rank: the row pass writes the slab's top half in place (send aliases it, the
+    all-to-all is skipped); the result is the whole square's."""
+    from celestia_eds.sharded import LocalComm, ShardedSquare
+    from sharded_oracle import OracleSteps
+    k = 8
+    ods = random_ods(k, 31)
+    sq = ShardedSquare(k, 0, 1, OracleSteps())
+    assert sq.send.data_ptr() == sq.slab.data_ptr()
+    sq.ods_rows.copy_(torch.from_numpy(ods))
+    if local:
+        LocalComm.run([sq])
+    else:
+        class NoComm:  # a one-rank communicator: the gathers are identities
+            def all_gather(self, out, inp):
+                out.copy_(inp)
+
+            def all_reduce_max(self, t):
+                pass
+
+            def all_to_all(self, out, inp):
+                raise AssertionError("one rank must not exchange")
+        sq.run(NoComm())
+    eds, rr, cr, dah = oracle.extend_and_commit(ods)
+    assert np.array_equal(sq.slab.numpy(), eds)
+    assert np.array_equal(sq.row_roots.numpy(), rr)
+    assert np.array_equal(sq.col_roots.numpy(), cr)
+    assert sq.dah.numpy().tobytes() == dah
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("k,n", [(256, 1), (256, 2), (256, 8), (512, 4), (512, 8)])
 def test_device_sharded_local(ctx, oracle, k, n):
