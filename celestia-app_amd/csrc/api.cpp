@@ -919,49 +919,76 @@ static cel_status encode_check(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_c
   return CEL_OK;
 }
 
-// rsmt2d solveCrossword's decode of `list` (incomplete axes of one direction): gathered,
-// decoded and scattered back into the square on the main stream; their encoding check
-// follows on the side stream. Nothing is synchronised: every flag is read back once at
-// the end of the repair.
-static cel_status solve_pass(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_col, const std::vector<int32_t>& list) {
+// rsmt2d solveCrossword's decode of `list` (incomplete axes of one direction), in two
+// halves so the host can put other side-stream work between them:
+//   solve_issue  the decode on the main stream (in place in the square, or gather ->
+//                decode -> scatter), then ev_main;
+//   solve_check  the encoding check of the solved axes on the side stream, after ev_main.
+// Nothing is synchronised: every flag is read back once at the end of the repair.
+struct Issued {
+  uint32_t na = 0;
+  uint32_t d = 0;
+  int32_t* idx = nullptr;
+};
+
+static cel_status solve_issue(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_col, const std::vector<int32_t>& list,
+                              Issued* out) {
   const Range range("repair.solve");
   const uint32_t W = 2 * k, na = (uint32_t)list.size();
+  out->na = na;
   if (!na) return CEL_OK;
-  const uint32_t d = b.solves++ & 1u;
-  uint8_t* dense = b.dense[d];
-  int32_t* idx;
+  const uint32_t d = out->d = b.solves++ & 1u;
   cel_status st;
-  if ((st = upload_list(ctx, b, list, b.main, &idx)) != CEL_OK) return st;
+  if ((st = upload_list(ctx, b, list, b.main, &out->idx)) != CEL_OK) return st;
+  const int32_t* idx = out->idx;
   hipError_t e;
   if (rs_decode_axis_supported(W, kShare)) {
     // register decoder in place: erased cells straight into the square (no gather /
-    // scatter on the chain); the side stream gathers the completed axes for their check
+    // scatter on the chain)
     if ((e = launch_rs_decode_in_square(b.eds, b.mask, W, idx, is_col, na, ctx->tables.mul8, b.main)) != hipSuccess ||
-        (e = hipEventRecord(b.ev_main, b.main)) != hipSuccess ||
-        (e = hipStreamWaitEvent(b.side, b.ev_main, 0)) != hipSuccess ||
-        (e = launch_gather_axes(b.eds, b.mask, W, idx, is_col, na, b.dchk, b.dmask_chk, b.side)) != hipSuccess)
+        (e = hipEventRecord(b.ev_main, b.main)) != hipSuccess)
       return hip_fail(ctx, e, "solve");
-    return encode_check(ctx, b, k, is_col, na, b.dchk, idx, b.side);
+    return CEL_OK;
   }
+  uint8_t* dense = b.dense[d];
   if ((e = hipStreamWaitEvent(b.main, b.ev_side[d], 0)) != hipSuccess ||  // the side stream is done with dense[d]
       (e = launch_gather_axes(b.eds, b.mask, W, idx, is_col, na, dense, b.dmask, b.main)) != hipSuccess ||
       (e = launch_rs_decode(dense, b.dmask, na, k, kShare, ctx->tables, nullptr, b.main)) != hipSuccess ||
       (e = launch_scatter_axes(b.eds, b.mask, W, idx, is_col, na, dense, b.main)) != hipSuccess ||
-      (e = hipEventRecord(b.ev_main, b.main)) != hipSuccess || (e = hipStreamWaitEvent(b.side, b.ev_main, 0)) != hipSuccess)
+      (e = hipEventRecord(b.ev_main, b.main)) != hipSuccess)
     return hip_fail(ctx, e, "solve");
-  if ((st = encode_check(ctx, b, k, is_col, na, dense, idx, b.side)) != CEL_OK) return st;
-  if ((e = hipEventRecord(b.ev_side[d], b.side)) != hipSuccess) return hip_fail(ctx, e, "event");
+  return CEL_OK;
+}
+
+// The side half of a solve_issue; ev_main must still be that solve's record.
+static cel_status solve_check(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_col, const Issued& s) {
+  if (!s.na) return CEL_OK;
+  const uint32_t W = 2 * k;
+  hipError_t e;
+  if ((e = hipStreamWaitEvent(b.side, b.ev_main, 0)) != hipSuccess) return hip_fail(ctx, e, "event");
+  if (rs_decode_axis_supported(W, kShare)) {  // the completed axes are gathered for their check
+    if ((e = launch_gather_axes(b.eds, b.mask, W, s.idx, is_col, s.na, b.dchk, b.dmask_chk, b.side)) != hipSuccess)
+      return hip_fail(ctx, e, "gather");
+    return encode_check(ctx, b, k, is_col, s.na, b.dchk, s.idx, b.side);
+  }
+  cel_status st;
+  if ((st = encode_check(ctx, b, k, is_col, s.na, b.dense[s.d], s.idx, b.side)) != CEL_OK) return st;
+  if ((e = hipEventRecord(b.ev_side[s.d], b.side)) != hipSuccess) return hip_fail(ctx, e, "event");
   return CEL_OK;
 }
 
 // Encoding check of complete axes (preRepairSanityCheck, and the orthogonal axes a solve
-// completed), on the side stream after the main stream's latest pass.
-static cel_status check_pass(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_col, const std::vector<int32_t>& list) {
+// completed) on the side stream. wait_main: after the main stream's latest work; without
+// it the caller guarantees the axes are final in the side stream's order already (the
+// orthogonal axes of a pass whose solve_check the side stream has passed).
+static cel_status check_pass(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_col, const std::vector<int32_t>& list,
+                             bool wait_main) {
   const Range range("repair.check");
   const uint32_t W = 2 * k, na = (uint32_t)list.size();
   if (!na) return CEL_OK;
   hipError_t e;
-  if ((e = hipEventRecord(b.ev_main, b.main)) != hipSuccess || (e = hipStreamWaitEvent(b.side, b.ev_main, 0)) != hipSuccess)
+  if (wait_main &&
+      ((e = hipEventRecord(b.ev_main, b.main)) != hipSuccess || (e = hipStreamWaitEvent(b.side, b.ev_main, 0)) != hipSuccess))
     return hip_fail(ctx, e, "event");
   int32_t* idx;
   cel_status st;
@@ -1116,7 +1143,11 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
     for (uint32_t j = 0; j < W; j++) c += r[j];
     if (c >= k && c < W) first.push_back((int32_t)i);
   }
-  if ((st = solve_pass(ctx, b, k, 0, first)) != CEL_OK) return st;
+  {
+    Issued s0;
+    if ((st = solve_issue(ctx, b, k, 0, first, &s0)) != CEL_OK || (st = solve_check(ctx, b, k, 0, s0)) != CEL_OK)
+      return st;
+  }
   bool first_issued = !first.empty();
   MaskBits mb(hm, W);
   std::vector<Check> order;
@@ -1131,8 +1162,13 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
           comp[is_col].push_back((int32_t)i);
         }
     for (int is_col = 0; is_col < 2; is_col++)
-      if ((st = check_pass(ctx, b, k, is_col, comp[is_col])) != CEL_OK) return st;
+      if ((st = check_pass(ctx, b, k, is_col, comp[is_col], true)) != CEL_OK) return st;
   }
+  // The orthogonal checks of a pass are issued after the next pass's decode (or the final
+  // commit), so the host's enqueue of them is not on the solve chain; the side stream runs
+  // them right after that pass's own encoding checks.
+  std::vector<int32_t> pending;
+  int pending_col = 0;
   // solveCrossword: all rows, then all columns, until solved or stuck
   bool solved = false;
   std::vector<std::vector<int32_t>> by_solve;
@@ -1148,8 +1184,13 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
       if (list.empty()) continue;
       if (first_issued) {  // the first row pass (the same list, issued above)
         first_issued = false;
-      } else if ((st = solve_pass(ctx, b, k, is_col, list)) != CEL_OK) {
-        return st;
+      } else {
+        Issued s1;
+        if ((st = solve_issue(ctx, b, k, is_col, list, &s1)) != CEL_OK ||
+            (st = check_pass(ctx, b, k, pending_col, pending, false)) != CEL_OK ||
+            (st = solve_check(ctx, b, k, is_col, s1)) != CEL_OK)
+          return st;
+        pending.clear();
       }
       // sequential view of the pass: solve i fills its missing cells, completing the
       // orthogonal axes whose last missing cell it held
@@ -1164,7 +1205,9 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
         solves.push_back({is_col, list[t]});
       }
       std::sort(orth.begin(), orth.end());
-      if ((st = check_pass(ctx, b, k, !is_col, orth)) != CEL_OK) return st;
+      if (!pending.empty() && (st = check_pass(ctx, b, k, pending_col, pending, false)) != CEL_OK) return st;
+      pending.swap(orth);
+      pending_col = !is_col;
       progress = true;
     }
     if (mb.total == cells) {
@@ -1180,6 +1223,7 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
   uint8_t* d_cr = b.roots + roots_b;
   if ((e = launch_commit(b.eds, k, 1, d_rr, d_cr, nullptr, nullptr, b.work, false, s)) != hipSuccess)
     return hip_fail(ctx, e, "roots");
+  if ((st = check_pass(ctx, b, k, pending_col, pending, false)) != CEL_OK) return st;
   if ((e = hipEventRecord(b.ev_done, b.side)) != hipSuccess || (e = hipStreamWaitEvent(s, b.ev_done, 0)) != hipSuccess)
     return hip_fail(ctx, e, "join");
   if ((e = hipMemcpyAsync(b.hres, b.roots, b.res_bytes, hipMemcpyDeviceToHost, s)) != hipSuccess)
