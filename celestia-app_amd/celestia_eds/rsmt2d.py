@@ -89,9 +89,15 @@ def NewLeoRSCodec():
     return LeoRSCodec()
 
 
-def _default_constructor(tree_constructor):
-    """True for None and for wrapper.NewConstructor(k) (served by the device pass)."""
-    return tree_constructor is None or getattr(tree_constructor, "_cel_wrapper_constructor", False)
+def _default_constructor(tree_constructor, width):
+    """True for None and for wrapper.NewConstructor(k) with k = width / 2 (served by the
+    device pass). A wrapper constructor for another square size builds trees with another
+    Q0 boundary (or fails to push, nmt_wrapper.go:93-99) upstream, so it is treated like
+    any caller constructor: its own trees give the roots."""
+    if tree_constructor is None:
+        return True
+    return (getattr(tree_constructor, "_cel_wrapper_constructor", False)
+            and getattr(tree_constructor, "square_size", None) == width // 2)
 
 
 class ExtendedDataSquare:
@@ -102,7 +108,7 @@ class ExtendedDataSquare:
         self._row_roots = row_roots
         self._col_roots = col_roots
         self._ctx = ctx
-        self._tree = None if _default_constructor(tree_constructor) else tree_constructor
+        self._tree = None if _default_constructor(tree_constructor, cells.shape[0]) else tree_constructor
 
     @property
     def ctx(self):
@@ -202,7 +208,7 @@ def ComputeExtendedDataSquare(data, codec=None, tree_constructor=None, ctx=None)
     from . import da
     _check_codec(codec)
     eds = da._extend(data, ctx=ctx, order_check=True)
-    if not _default_constructor(tree_constructor):
+    if not _default_constructor(tree_constructor, eds.Width()):
         eds._row_roots = eds._col_roots = None
         eds._tree = tree_constructor
     return eds

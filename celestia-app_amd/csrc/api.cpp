@@ -156,6 +156,7 @@ const char* cel_strerror(cel_status st) {
     case CEL_ESHORT: return "data is too short to contain namespace ID";
     case CEL_EPUSHPAST: return "pushed past predetermined square size";
     case CEL_EBADROOT: return "bad root input";
+    case CEL_ENODATA: return "no shard data";
     default: return "unknown status";
   }
 }
@@ -523,7 +524,7 @@ cel_status cel_codec_encode(cel_ctx* ctx, const uint8_t* data, uint32_t n, uint3
   if (cel_codec_validate_chunk_size(len)) return fail(ctx, CEL_ECHUNK, "shard size must be a multiple of 64");
   if (!is_pow2(n)) return fail(ctx, CEL_ENOTPOW2, "number of data shards is not a power of 2");
   if (n > kMaxGf16Width) return fail(ctx, CEL_ETOOBIG, "too many shards for the device path");
-  if (len == 0) return CEL_OK;  // empty shards: empty parity
+  if (len == 0) return fail(ctx, CEL_ENODATA, "no shard data");  // klauspost ErrShardNoData
   DeviceGuard g(ctx->device);
   hipError_t e = hipSuccess;
   const size_t b = (size_t)n * len;
@@ -557,9 +558,9 @@ cel_status cel_codec_decode(cel_ctx* ctx, uint8_t* shards, const uint8_t* presen
   if (n > 1024) return fail(ctx, CEL_ETOOBIG, "too many shards for the device decoder");
   uint32_t have = 0;
   for (uint32_t i = 0; i < 2 * n; i++) have += present[i] ? 1 : 0;
+  if (len == 0) return fail(ctx, CEL_ENODATA, "no shard data");  // klauspost ErrShardNoData
   if (have == 2 * n) return CEL_OK;
   if (have < n) return fail(ctx, CEL_ETOOFEW, "too few shards given");
-  if (len == 0) return CEL_OK;
   DeviceGuard g(ctx->device);
   hipError_t e = hipSuccess;
   const size_t b = (size_t)2 * n * len;
@@ -893,6 +894,17 @@ static cel_status upload_list(cel_ctx* ctx, RepairBufs& b, const std::vector<int
   return CEL_OK;
 }
 
+// Randomised idle time in front of an enqueue point (cel_debug_schedule_fuzz; off = 0).
+static cel_status fuzz(cel_ctx* ctx, hipStream_t s) {
+  if (!ctx->fuzz_max_us) return CEL_OK;
+  uint64_t x = (ctx->fuzz_state += 0x9E3779B97F4A7C15ull);  // splitmix64
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  const hipError_t e = launch_delay((uint32_t)(x % (ctx->fuzz_max_us + 1ull)), s);
+  return e == hipSuccess ? CEL_OK : hip_fail(ctx, e, "delay");
+}
+
 // Re-encode check of na gathered axes at `dense` on stream s: the data half of each axis
 // is encoded again and compared with its parity half; mismatches set flags[is_col*W + axis].
 static cel_status encode_check(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_col, uint32_t na, const uint8_t* dense,
@@ -939,7 +951,7 @@ static cel_status solve_issue(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_co
   if (!na) return CEL_OK;
   const uint32_t d = out->d = b.solves++ & 1u;
   cel_status st;
-  if ((st = upload_list(ctx, b, list, b.main, &out->idx)) != CEL_OK) return st;
+  if ((st = upload_list(ctx, b, list, b.main, &out->idx)) != CEL_OK || (st = fuzz(ctx, b.main)) != CEL_OK) return st;
   const int32_t* idx = out->idx;
   hipError_t e;
   if (rs_decode_axis_supported(W, kShare)) {
@@ -966,12 +978,13 @@ static cel_status solve_check(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_co
   const uint32_t W = 2 * k;
   hipError_t e;
   if ((e = hipStreamWaitEvent(b.side, b.ev_main, 0)) != hipSuccess) return hip_fail(ctx, e, "event");
+  cel_status st;
+  if ((st = fuzz(ctx, b.side)) != CEL_OK) return st;
   if (rs_decode_axis_supported(W, kShare)) {  // the completed axes are gathered for their check
     if ((e = launch_gather_axes(b.eds, b.mask, W, s.idx, is_col, s.na, b.dchk, b.dmask_chk, b.side)) != hipSuccess)
       return hip_fail(ctx, e, "gather");
     return encode_check(ctx, b, k, is_col, s.na, b.dchk, s.idx, b.side);
   }
-  cel_status st;
   if ((st = encode_check(ctx, b, k, is_col, s.na, b.dense[s.d], s.idx, b.side)) != CEL_OK) return st;
   if ((e = hipEventRecord(b.ev_side[s.d], b.side)) != hipSuccess) return hip_fail(ctx, e, "event");
   return CEL_OK;
@@ -992,7 +1005,7 @@ static cel_status check_pass(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_col
     return hip_fail(ctx, e, "event");
   int32_t* idx;
   cel_status st;
-  if ((st = upload_list(ctx, b, list, b.side, &idx)) != CEL_OK) return st;
+  if ((st = upload_list(ctx, b, list, b.side, &idx)) != CEL_OK || (st = fuzz(ctx, b.side)) != CEL_OK) return st;
   if ((e = launch_gather_axes(b.eds, b.mask, W, idx, is_col, na, b.dchk, b.dmask_chk, b.side)) != hipSuccess)
     return hip_fail(ctx, e, "gather");
   return encode_check(ctx, b, k, is_col, na, b.dchk, idx, b.side);
@@ -1111,12 +1124,259 @@ struct MaskBits {
   }
 };
 
+// The final verification's results, read back in one copy: every root of the square and
+// the encoding-check flags by (direction, axis).
+struct Verify {
+  const uint8_t* got;  // [2][W][90]
+  const int32_t* flags;
+  const uint8_t *row_roots, *col_roots;
+  uint32_t W;
+  bool root_ok(int is_col, int32_t i) const {
+    const uint8_t* exp = (is_col ? col_roots : row_roots) + (size_t)i * kNode;
+    return std::memcmp(got + (size_t)is_col * W * kNode + (size_t)i * kNode, exp, kNode) == 0;
+  }
+  bool enc_ok(int is_col, int32_t i) const { return flags[(size_t)is_col * W + i] == 0; }
+  // rsmt2d's order of checks: the first that fails (index into order, -1 if none) and
+  // its status
+  long first_failure(const std::vector<Check>& order, cel_status* code) const {
+    for (size_t t = 0; t < order.size(); t++) {
+      const Check& c = order[t];
+      bool ok = true;
+      *code = CEL_EBYZANTINE;
+      switch (c.kind) {
+        case Check::SANITY:
+          if (!root_ok(c.is_col, c.idx)) {
+            *code = CEL_EBADROOT;
+            ok = false;
+          } else {
+            ok = enc_ok(c.is_col, c.idx);
+          }
+          break;
+        case Check::SOLVE: ok = enc_ok(c.is_col, c.idx) && root_ok(c.is_col, c.idx); break;
+        case Check::ORTH: ok = root_ok(c.is_col, c.idx) && enc_ok(c.is_col, c.idx); break;
+      }
+      if (!ok) return (long)t;
+    }
+    return -1;
+  }
+};
+
+// hm := the presence mask before solve `upto` of `solves` (each solve completes its axis)
+static void rollback(std::vector<uint8_t>& hm, uint32_t W, const std::vector<Solve>& solves, size_t upto) {
+  for (size_t t = 0; t < upto; t++) {
+    const uint32_t i = (uint32_t)solves[t].idx;
+    if (solves[t].is_col)
+      for (uint32_t j = 0; j < W; j++) hm[(size_t)j * W + i] = 1;
+    else
+      std::memset(hm.data() + (size_t)i * W, 1, W);
+  }
+}
+
+// Report a failing axis: status, axis, index, and for CEL_EBYZANTINE rsmt2d's
+// ErrByzantineData.Shares: the axis's cells from the square (complete axes never change;
+// cells of a solved axis present before its solve kept their bytes), with the axis's mask
+// from hm (masked: hm is rolled back to the mask before the failing solve) or all present.
+static cel_status fail_axis(cel_ctx* ctx, const RepairBufs& b, const std::vector<uint8_t>& hm, const RepairOut& out,
+                            cel_status code, int is_col, int32_t idx, bool masked) {
+  const uint32_t W = b.W;
+  if (out.bad_axis) *out.bad_axis = is_col;
+  if (out.bad_index) *out.bad_index = idx;
+  if (code == CEL_EBYZANTINE && (out.byz_shares || out.byz_present)) {
+    std::vector<uint8_t> axis((size_t)W * kShare);
+    const uint8_t* src = b.eds + (is_col ? (size_t)idx * kShare : (size_t)idx * W * kShare);
+    const hipError_t ce = is_col ? hipMemcpy2D(axis.data(), kShare, src, (size_t)W * kShare, kShare, W,
+                                                hipMemcpyDeviceToHost)
+                                 : hipMemcpy(axis.data(), src, axis.size(), hipMemcpyDeviceToHost);
+    if (ce != hipSuccess) return hip_fail(ctx, ce, "byzantine shares");
+    for (uint32_t j = 0; j < W; j++) {
+      const uint8_t p = masked ? hm[is_col ? (size_t)j * W + (uint32_t)idx : (size_t)idx * W + j] : 1;
+      if (out.byz_present) out.byz_present[j] = p;
+      if (out.byz_shares) {
+        if (p) std::memcpy(out.byz_shares + (size_t)j * kShare, axis.data() + (size_t)j * kShare, kShare);
+        else std::memset(out.byz_shares + (size_t)j * kShare, 0, kShare);
+      }
+    }
+  }
+  const char* dir = is_col ? "col" : "row";
+  return fail(ctx, code, code == CEL_EBADROOT
+                             ? std::string("bad root input: ") + dir + " " + std::to_string(idx)
+                             : std::string("byzantine ") + (is_col ? "column" : "row") + " " + std::to_string(idx));
+}
+
+// Commit every root of the square on the main stream beside the side stream's last checks,
+// join the streams and read roots and flags back (one page-locked copy).
+static cel_status verify_square(cel_ctx* ctx, RepairBufs& b, uint32_t k, int pending_col,
+                                const std::vector<int32_t>& pending, Verify* v) {
+  const uint32_t W = 2 * k;
+  const size_t roots_b = (size_t)W * kNode;
+  hipError_t e;
+  cel_status st;
+  if ((st = fuzz(ctx, b.main)) != CEL_OK) return st;
+  if ((e = launch_commit(b.eds, k, 1, b.roots, b.roots + roots_b, nullptr, nullptr, b.work, false, b.main)) !=
+      hipSuccess)
+    return hip_fail(ctx, e, "roots");
+  if ((st = check_pass(ctx, b, k, pending_col, pending, false)) != CEL_OK) return st;
+  if ((e = hipEventRecord(b.ev_done, b.side)) != hipSuccess || (e = hipStreamWaitEvent(b.main, b.ev_done, 0)) != hipSuccess)
+    return hip_fail(ctx, e, "join");
+  if ((e = hipMemcpyAsync(b.hres, b.roots, b.res_bytes, hipMemcpyDeviceToHost, b.main)) != hipSuccess)
+    return hip_fail(ctx, e, "D2H");
+  if ((e = hipStreamSynchronize(b.main)) != hipSuccess) return hip_fail(ctx, e, "sync");
+  v->got = b.hres;
+  v->flags = reinterpret_cast<const int32_t*>(b.hres + (b.res_bytes - 2 * (size_t)W * 4));
+  v->W = W;
+  return CEL_OK;
+}
+
+// rsmt2d's own solve order, for a square the pass-parallel schedule found byzantine.
+//
+// solveCrossword sweeps `for i { solveCrosswordRow(i); solveCrosswordCol(i) }`, and on
+// inconsistent data which axis fails first, and with which Shares, depends on that order.
+// The host replays the sweeps over the mask alone (every solve completes its axis): the
+// solve sequence, the orthogonal axes each solve completes, and each solve's level, one
+// more than the highest level among the solves that filled a cell it reads. Solves of one
+// level touch no cell another of them fills, so a level runs as one row and one column
+// launch; level by level the device sees every axis exactly as rsmt2d's sequence does.
+// hm0: the mask the repair started from; cells present in it still hold their bytes
+// (every decoder stores erased cells only).
+static cel_status repair_exact(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>& hm, uint32_t k, const Verify& base,
+                               const RepairOut& out) {
+  const Range range("repair.exact");
+  const uint32_t W = 2 * k;
+  const size_t cells = (size_t)W * W;
+  std::vector<uint8_t> m(hm);
+  std::vector<uint32_t> cnt[2] = {std::vector<uint32_t>(W, 0), std::vector<uint32_t>(W, 0)};
+  size_t total = 0;
+  for (uint32_t i = 0; i < W; i++)
+    for (uint32_t j = 0; j < W; j++)
+      if (m[(size_t)i * W + j]) {
+        cnt[0][i]++;
+        cnt[1][j]++;
+        total++;
+      }
+  std::vector<int32_t> lvl_of(cells, 0);
+  std::vector<Solve> solves;
+  std::vector<int32_t> level;
+  std::vector<Check> order;
+  int32_t nlevels = 0;
+  bool solved = total == cells;
+  while (!solved) {
+    bool progress = false;
+    for (uint32_t i = 0; i < W; i++)
+      for (int d = 0; d < 2; d++) {
+        if (cnt[d][i] == W || cnt[d][i] < k) continue;
+        const size_t base_c = d ? i : (size_t)i * W, step = d ? W : 1;
+        int32_t L = 0;
+        for (uint32_t j = 0; j < W; j++) {
+          const size_t c = base_c + j * step;
+          if (m[c] && lvl_of[c] > L) L = lvl_of[c];
+        }
+        L++;
+        const int32_t si = (int32_t)solves.size();
+        order.push_back({Check::SOLVE, d, (int32_t)i, si});
+        for (uint32_t j = 0; j < W; j++) {
+          const size_t c = base_c + j * step;
+          if (m[c]) continue;
+          if (cnt[!d][j] == W - 1) order.push_back({Check::ORTH, !d, (int32_t)j, si});
+          m[c] = 1;
+          lvl_of[c] = L;
+          cnt[!d][j]++;
+          total++;
+        }
+        cnt[d][i] = W;
+        solves.push_back({d, (int32_t)i});
+        level.push_back(L);
+        if (L > nlevels) nlevels = L;
+        progress = true;
+      }
+    if (total == cells) solved = true;
+    if (!progress) break;
+  }
+  // device: the starting mask again, every level's axis lists in one upload (each axis is
+  // solved once: at most 2W entries), then the levels in order on the main stream
+  std::vector<int32_t> lists;
+  struct Group {
+    uint32_t off, n;
+    int is_col;
+  };
+  std::vector<Group> groups;
+  {
+    std::vector<std::vector<int32_t>> by[2];
+    by[0].resize(nlevels + 1);
+    by[1].resize(nlevels + 1);
+    for (size_t t = 0; t < solves.size(); t++) by[solves[t].is_col][level[t]].push_back(solves[t].idx);
+    for (int32_t L = 1; L <= nlevels; L++)
+      for (int d = 0; d < 2; d++)
+        if (!by[d][L].empty()) {
+          groups.push_back({(uint32_t)lists.size(), (uint32_t)by[d][L].size(), d});
+          lists.insert(lists.end(), by[d][L].begin(), by[d][L].end());
+        }
+  }
+  hipError_t e;
+  cel_status st;
+  // both streams are idle (verify_square synchronised the joined streams)
+  std::memcpy(b.hmask, hm.data(), cells);
+  std::memcpy(b.hidx, lists.data(), lists.size() * 4);
+  b.slot = (uint32_t)((lists.size() + W - 1) / W);  // the slots the lists occupy
+  if ((e = hipMemcpyAsync(b.mask, b.hmask, cells, hipMemcpyHostToDevice, b.main)) != hipSuccess ||
+      (!lists.empty() && (e = hipMemcpyAsync(b.idx, b.hidx, lists.size() * 4, hipMemcpyHostToDevice, b.main)) != hipSuccess) ||
+      (e = hipMemsetAsync(b.flags, 0, 2 * (size_t)W * 4, b.main)) != hipSuccess)
+    return hip_fail(ctx, e, "H2D");
+  const bool in_square = rs_decode_axis_supported(W, kShare);
+  for (const Group& g : groups) {
+    const int32_t* idx = b.idx + g.off;
+    if ((st = fuzz(ctx, b.main)) != CEL_OK) return st;
+    if (in_square) {
+      e = launch_rs_decode_in_square(b.eds, b.mask, W, idx, g.is_col, g.n, ctx->tables.mul8, b.main);
+    } else if ((e = launch_gather_axes(b.eds, b.mask, W, idx, g.is_col, g.n, b.dense[0], b.dmask, b.main)) ==
+                   hipSuccess &&
+               (e = launch_rs_decode(b.dense[0], b.dmask, g.n, k, kShare, ctx->tables, nullptr, b.main)) ==
+                   hipSuccess) {
+      e = launch_scatter_axes(b.eds, b.mask, W, idx, g.is_col, g.n, b.dense[0], b.main);
+    }
+    if (e != hipSuccess) return hip_fail(ctx, e, "solve");
+  }
+  // encoding checks of every axis complete at the end (the sanity axes passed already and
+  // pass again), on the side stream after the last level
+  if ((e = hipEventRecord(b.ev_main, b.main)) != hipSuccess || (e = hipStreamWaitEvent(b.side, b.ev_main, 0)) != hipSuccess)
+    return hip_fail(ctx, e, "event");
+  std::vector<int32_t> comp[2];
+  for (int d = 0; d < 2; d++)
+    for (uint32_t i = 0; i < W; i++)
+      if (cnt[d][i] == W) comp[d].push_back((int32_t)i);
+  if ((st = check_pass(ctx, b, k, 0, comp[0], false)) != CEL_OK) return st;
+  Verify v = base;
+  if ((st = verify_square(ctx, b, k, 1, comp[1], &v)) != CEL_OK) return st;
+  cel_status code;
+  const long f = v.first_failure(order, &code);
+  if (f >= 0) {
+    const Check& c = order[(size_t)f];
+    rollback(hm, W, solves, (size_t)c.solve);
+    return fail_axis(ctx, b, hm, out, code, c.is_col, c.idx, c.kind == Check::SOLVE);
+  }
+  // not reached for a square the pass schedule found byzantine (the outcome does not depend
+  // on the order when every check passes), kept for completeness
+  if (!solved) {
+    rollback(hm, W, solves, solves.size());
+    return fail(ctx, CEL_EUNREPAIRABLE, "failed to solve data square");
+  }
+  std::fill(hm.begin(), hm.end(), (uint8_t)1);
+  return CEL_OK;
+}
+
 // rsmt2d Repair over the EDS resident at b.eds. hm = host presence mask (updated: all
 // ones on success, the mask before the failing solve on a byzantine / bad-root error,
 // the mask after the last solve when stuck). No pass waits for the device. Root checks
 // are deferred: an axis, once complete, never changes, so one commit pass over the final
 // square gives every root rsmt2d checks on the way, and the checks are replayed in
 // rsmt2d's order, reporting the first failure.
+//
+// The solves run in passes (every solvable row, then every solvable column, ...), which
+// decodes whole directions at once. When every check passes, the outcome equals that of
+// rsmt2d's sweep order (row i, then column i): all cells of the final square then agree
+// with valid codewords whose roots match, so any order decodes the same bytes and passes
+// the same checks, and the set of axes that can be solved is the same closure. Only a
+// failing solve or orthogonal check depends on the order; that square is replayed in
+// rsmt2d's order by repair_exact.
 static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>& hm, uint32_t k,
                               const uint8_t* row_roots, const uint8_t* col_roots, const RepairOut& out) {
   const uint32_t W = 2 * k;
@@ -1169,7 +1429,7 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
   // them right after that pass's own encoding checks.
   std::vector<int32_t> pending;
   int pending_col = 0;
-  // solveCrossword: all rows, then all columns, until solved or stuck
+  // passes: all solvable rows, then all solvable columns, until solved or stuck
   bool solved = false;
   std::vector<std::vector<int32_t>> by_solve;
   for (;;) {
@@ -1216,85 +1476,17 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
     }
     if (!progress) break;
   }
-  // every root of the (possibly partial) square in one commit pass, roots only, beside
-  // the side stream's last checks; then both streams join
-  const size_t roots_b = (size_t)W * kNode;
-  uint8_t* d_rr = b.roots;
-  uint8_t* d_cr = b.roots + roots_b;
-  if ((e = launch_commit(b.eds, k, 1, d_rr, d_cr, nullptr, nullptr, b.work, false, s)) != hipSuccess)
-    return hip_fail(ctx, e, "roots");
-  if ((st = check_pass(ctx, b, k, pending_col, pending, false)) != CEL_OK) return st;
-  if ((e = hipEventRecord(b.ev_done, b.side)) != hipSuccess || (e = hipStreamWaitEvent(s, b.ev_done, 0)) != hipSuccess)
-    return hip_fail(ctx, e, "join");
-  if ((e = hipMemcpyAsync(b.hres, b.roots, b.res_bytes, hipMemcpyDeviceToHost, s)) != hipSuccess)
-    return hip_fail(ctx, e, "D2H");
-  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "sync");
-  const uint8_t* got = b.hres;
-  const int32_t* flags = reinterpret_cast<const int32_t*>(b.hres + (b.res_bytes - 2 * (size_t)W * 4));
-  auto root_ok = [&](int is_col, int32_t i) {
-    const uint8_t* exp = (is_col ? col_roots : row_roots) + (size_t)i * kNode;
-    return std::memcmp(got + is_col * roots_b + (size_t)i * kNode, exp, kNode) == 0;
-  };
-  auto enc_ok = [&](int is_col, int32_t i) { return flags[(size_t)is_col * W + i] == 0; };
-  // hm := the presence mask before solve `upto` (all solves before it applied)
-  auto rollback = [&](size_t upto) {
-    for (size_t t = 0; t < upto; t++) {
-      const uint32_t i = (uint32_t)solves[t].idx;
-      if (solves[t].is_col)
-        for (uint32_t j = 0; j < W; j++) hm[(size_t)j * W + i] = 1;
-      else
-        std::memset(hm.data() + (size_t)i * W, 1, W);
-    }
-  };
-  auto fail_axis = [&](cel_status code, int is_col, int32_t idx, bool masked) {
-    if (out.bad_axis) *out.bad_axis = is_col;
-    if (out.bad_index) *out.bad_index = idx;
-    if (code == CEL_EBYZANTINE && (out.byz_shares || out.byz_present)) {
-      // ErrByzantineData.Shares: the axis's cells from the square (complete axes never
-      // change; cells of a solved axis present before its solve kept their bytes), with
-      // the axis's mask before its solve (hm is rolled back to it)
-      std::vector<uint8_t> axis((size_t)W * kShare);
-      const uint8_t* src = b.eds + (is_col ? (size_t)idx * kShare : (size_t)idx * W * kShare);
-      const hipError_t ce = is_col ? hipMemcpy2D(axis.data(), kShare, src, (size_t)W * kShare, kShare, W,
-                                                  hipMemcpyDeviceToHost)
-                                   : hipMemcpy(axis.data(), src, axis.size(), hipMemcpyDeviceToHost);
-      if (ce != hipSuccess) return hip_fail(ctx, ce, "byzantine shares");
-      for (uint32_t j = 0; j < W; j++) {
-        const uint8_t p = masked ? hm[is_col ? (size_t)j * W + (uint32_t)idx : (size_t)idx * W + j] : 1;
-        if (out.byz_present) out.byz_present[j] = p;
-        if (out.byz_shares) {
-          if (p) std::memcpy(out.byz_shares + (size_t)j * kShare, axis.data() + (size_t)j * kShare, kShare);
-          else std::memset(out.byz_shares + (size_t)j * kShare, 0, kShare);
-        }
-      }
-    }
-    const char* dir = is_col ? "col" : "row";
-    return fail(ctx, code, code == CEL_EBADROOT
-                               ? std::string("bad root input: ") + dir + " " + std::to_string(idx)
-                               : std::string("byzantine ") + (is_col ? "column" : "row") + " " + std::to_string(idx));
-  };
-  for (const Check& c : order) {
-    switch (c.kind) {
-      case Check::SANITY:
-        if (!root_ok(c.is_col, c.idx)) return fail_axis(CEL_EBADROOT, c.is_col, c.idx, false);
-        if (!enc_ok(c.is_col, c.idx)) return fail_axis(CEL_EBYZANTINE, c.is_col, c.idx, false);
-        break;
-      case Check::SOLVE:
-        if (!enc_ok(c.is_col, c.idx) || !root_ok(c.is_col, c.idx)) {
-          rollback((size_t)c.solve);
-          return fail_axis(CEL_EBYZANTINE, c.is_col, c.idx, true);
-        }
-        break;
-      case Check::ORTH:
-        if (!root_ok(c.is_col, c.idx) || !enc_ok(c.is_col, c.idx)) {
-          rollback((size_t)c.solve);
-          return fail_axis(CEL_EBYZANTINE, c.is_col, c.idx, false);
-        }
-        break;
-    }
+  Verify v{nullptr, nullptr, row_roots, col_roots, W};
+  if ((st = verify_square(ctx, b, k, pending_col, pending, &v)) != CEL_OK) return st;
+  cel_status code;
+  const long f = v.first_failure(order, &code);
+  if (f >= 0) {
+    const Check& c = order[(size_t)f];
+    if (c.kind == Check::SANITY) return fail_axis(ctx, b, hm, out, code, c.is_col, c.idx, false);
+    return repair_exact(ctx, b, hm, k, v, out);
   }
   if (!solved) {
-    rollback(solves.size());
+    rollback(hm, W, solves, solves.size());
     return fail(ctx, CEL_EUNREPAIRABLE, "failed to solve data square");
   }
   std::fill(hm.begin(), hm.end(), (uint8_t)1);
@@ -1381,6 +1573,15 @@ cel_status cel_repair(cel_ctx* ctx, uint8_t* eds, uint8_t* present, uint32_t k, 
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "sync");
   std::memcpy(present, hm.data(), cells);
   return st;
+}
+
+cel_status cel_debug_schedule_fuzz(cel_ctx* ctx, uint64_t seed, uint32_t max_us) {
+  if (!ctx) return CEL_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (max_us > 100000) return fail(ctx, CEL_EINVAL, "max_us above 100 ms");
+  ctx->fuzz_state = seed;
+  ctx->fuzz_max_us = max_us;
+  return CEL_OK;
 }
 
 cel_status cel_dev_repair(cel_ctx* ctx, void* d_eds, uint8_t* present, uint32_t k, const uint8_t* row_roots,

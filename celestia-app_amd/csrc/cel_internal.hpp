@@ -124,6 +124,8 @@ hipError_t launch_scatter_axes(uint8_t* eds, uint8_t* mask, uint32_t W, const in
 hipError_t launch_cmp(const uint8_t* x, uint64_t xstride, const uint8_t* y, uint64_t ystride, uint64_t bytes,
                       uint32_t naxes, int32_t* flags, hipStream_t s, const int32_t* idx = nullptr);
 size_t axes_roots_workspace_size(uint32_t k, uint32_t naxes);
+// A single-wave kernel that idles `us` microseconds on s (schedule fuzzing only).
+hipError_t launch_delay(uint32_t us, hipStream_t s);
 hipError_t launch_axes_roots(const uint8_t* cells, uint32_t k, const int32_t* axis_idx, uint32_t naxes,
                              uint32_t* roots, void* work, hipStream_t s);
 
@@ -182,4 +184,8 @@ struct cel_ctx {
   // Grow-only page-locked host staging (the repair's axis lists).
   void* hstage = nullptr;
   size_t hstage_size = 0;
+  // Schedule fuzzing of the repair's two streams (cel_debug_schedule_fuzz; tests only):
+  // before each enqueue point, an idle kernel of 0..fuzz_max_us microseconds.
+  uint64_t fuzz_state = 0;
+  uint32_t fuzz_max_us = 0;
 };

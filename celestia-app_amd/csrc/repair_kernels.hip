@@ -55,6 +55,19 @@ __global__ __launch_bounds__(256) void k_cmp(const uint8_t* __restrict__ x, uint
   if (u.x != v.x || u.y != v.y || u.z != v.z || u.w != v.w) atomicOr(flags + (idx ? idx[a] : (int32_t)a), 1);
 }
 
+// Schedule fuzzing (cel_debug_schedule_fuzz): one wave that idles for `ticks` of the
+// 100 MHz constant clock, so a stream's next operation starts later. The loop reads only
+// the clock, so it always ends.
+__global__ __launch_bounds__(64) void k_delay(uint64_t ticks) {
+  const uint64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+hipError_t launch_delay(uint32_t us, hipStream_t s) {
+  hipLaunchKernelGGL(k_delay, dim3(1), dim3(64), 0, s, (uint64_t)us * 100u);
+  return hipGetLastError();
+}
+
 hipError_t launch_gather_axes(const uint8_t* eds, const uint8_t* mask, uint32_t W, const int32_t* idx, int is_col,
                               uint32_t naxes, uint8_t* dense, uint8_t* dmask, hipStream_t s) {
   const uint64_t total = (uint64_t)naxes * W * (kShare / 16);

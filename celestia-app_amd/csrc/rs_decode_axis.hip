@@ -357,6 +357,9 @@ hipError_t launch_rs_decode_axis(uint8_t* shards, const uint8_t* present, uint32
 
 hipError_t launch_rs_decode_in_square(uint8_t* eds, uint8_t* mask, uint32_t W, const int32_t* idx, int is_col,
                                       uint32_t naxes, const uint32_t* mul8, hipStream_t s) {
+  // One workgroup (blockIdx.y == 0) per axis reads and marks its presence: a cell wider
+  // than 4 slices of 128 B would add y-blocks whose presence reads race that mark.
+  static_assert(kShare <= 4 * 128, "in-square decode: one y-block per axis");
   if (!rs_decode_axis_supported(W, kShare) || (uint64_t)W * W * kShare >= 0x7fffffffull) return hipErrorInvalidValue;
   if (naxes == 0) return hipSuccess;
   return decode_axes(eds, mask, naxes, W, kShare, mul8, idx, W, is_col, s);

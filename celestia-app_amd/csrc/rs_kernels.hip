@@ -606,10 +606,13 @@ __global__ __launch_bounds__(256) void k_rs_decode(uint8_t* shards, const uint8_
   for (uint32_t chunk = blockIdx.y; chunk < len / 64u; chunk += gridDim.y) {
     const uint32_t coff = chunk * 64u;
     __syncthreads();  // the previous chunk's stores have read the LDS image
+    // erased points enter the transform as zero (work[i] = 0), whatever bytes the
+    // caller's buffer holds there ("missing cells may hold anything")
     for (uint32_t it = threadIdx.x; it < n * 4; it += blockDim.x) {
       const uint32_t p = it >> 2, q = it & 3;
       const uint32_t r = p < m ? m + p : p - m;
-      reinterpret_cast<uint4*>(lds)[it] = reinterpret_cast<const uint4*>(axis + (uint64_t)r * len + coff)[q];
+      reinterpret_cast<uint4*>(lds)[it] =
+          pres[p] ? reinterpret_cast<const uint4*>(axis + (uint64_t)r * len + coff)[q] : uint4{0, 0, 0, 0};
     }
     __syncthreads();
     if (GF16) {

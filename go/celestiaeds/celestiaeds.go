@@ -27,6 +27,8 @@ import (
 	"sync"
 	"unsafe"
 
+	"github.com/celestiaorg/celestia-app/v3/pkg/appconsts"
+	"github.com/celestiaorg/celestia-app/v3/pkg/wrapper"
 	"github.com/celestiaorg/rsmt2d"
 )
 
@@ -39,8 +41,31 @@ const (
 
 // Status codes map onto the reference's Go errors (include/celestia_eds.h):
 // CEL_EBYZANTINE -> *rsmt2d.ErrByzantineData, CEL_EUNREPAIRABLE ->
-// rsmt2d.ErrUnrepairableDataSquare, the rest -> errors carrying the reference's message.
+// rsmt2d.ErrUnrepairableDataSquare, the rest -> a *StatusError carrying the reference's
+// message (errors.Is(err, ErrNotPow2) for CEL_ENOTPOW2).
 var ErrNotPow2 = errors.New("number of shares is not a power of 2")
+
+// StatusError is a failing cel_* call: its status code and cel_last_error's message.
+type StatusError struct {
+	Status int
+	Msg    string
+}
+
+func (e *StatusError) Error() string { return e.Msg }
+
+func (e *StatusError) Unwrap() error {
+	if e.Status == C.CEL_ENOTPOW2 {
+		return ErrNotPow2
+	}
+	return nil
+}
+
+// tooBig reports whether err is CEL_ETOOBIG: a square or codeword wider than the device
+// path. Those calls are answered by the reference path instead (INTEGRATION.md §1).
+func tooBig(err error) bool {
+	var se *StatusError
+	return errors.As(err, &se) && se.Status == C.CEL_ETOOBIG
+}
 
 type Context struct {
 	mu  sync.Mutex
@@ -70,24 +95,25 @@ func (c *Context) errLocked(st C.cel_status) error {
 	if st == C.CEL_OK {
 		return nil
 	}
-	msg := C.GoString(C.cel_last_error(c.ctx))
-	switch st {
-	case C.CEL_ENOTPOW2:
-		return fmt.Errorf("%w: %s", ErrNotPow2, msg)
-	case C.CEL_EUNREPAIRABLE:
+	if st == C.CEL_EUNREPAIRABLE {
 		return rsmt2d.ErrUnrepairableDataSquare
 	}
-	return errors.New(msg)
+	return &StatusError{Status: int(st), Msg: C.GoString(C.cel_last_error(c.ctx))}
 }
 
 // ExtendShares is the device pass behind da.ExtendShares: the [][]byte ODS is copied
 // into one contiguous buffer (cgo may not retain Go pointers), extended on the GPU, and
-// the flattened EDS plus all 4k roots and the DAH hash come back in one call.
-// The caller wraps the result with rsmt2d.ImportExtendedDataSquare(flat, codec,
-// RootTableConstructor(rowRoots, colRoots)) so NewDataAvailabilityHeader is unchanged.
-// Only the parity cells cross PCIe (CEL_FLAG_PARITY_ONLY): flat's Q0 cells are left
-// zero, ExtendSquare points them at the input shares.
+// the whole flattened EDS (Q0 included) plus all 4k roots and the DAH hash come back in
+// one call. A caller can wrap flat with rsmt2d.ImportExtendedDataSquare(cells of flat,
+// codec, (&RootTable{...}).NewTree). ExtendSquare does that with less PCIe traffic.
 func (c *Context) ExtendShares(shares [][]byte) (flat []byte, rowRoots, colRoots [][]byte, dah []byte, err error) {
+	return c.extend(shares, flagOrder)
+}
+
+// extend runs cel_extend_shares with flags. With flagParity only the parity cells cross
+// PCIe and flat's Q0 cells stay zero: the caller points them at the input shares.
+func (c *Context) extend(shares [][]byte, flags C.uint32_t) (flat []byte, rowRoots, colRoots [][]byte, dah []byte,
+	err error) {
 	n := len(shares)
 	buf := C.malloc(C.size_t(n * ShareSize))
 	defer C.free(buf)
@@ -107,7 +133,7 @@ func (c *Context) ExtendShares(shares [][]byte) (flat []byte, rowRoots, colRoots
 	err = c.call(func() C.cel_status {
 		return C.cel_extend_shares(c.ctx, (*C.uint8_t)(buf), C.uint32_t(n), ShareSize,
 			(*C.uint8_t)(unsafe.Pointer(&flat[0])), (*C.uint8_t)(unsafe.Pointer(&rr[0])),
-			(*C.uint8_t)(unsafe.Pointer(&cr[0])), (*C.uint8_t)(unsafe.Pointer(&dah[0])), flagOrder|flagParity)
+			(*C.uint8_t)(unsafe.Pointer(&cr[0])), (*C.uint8_t)(unsafe.Pointer(&dah[0])), flags)
 	})
 	if err != nil {
 		return nil, nil, nil, nil, err
@@ -123,11 +149,21 @@ func (c *Context) ExtendShares(shares [][]byte) (flat []byte, rowRoots, colRoots
 // the same power-of-two check and error, then one device pass, and an
 // *rsmt2d.ExtendedDataSquare imported with a RootTable constructor, so
 // da.NewDataAvailabilityHeader's eds.RowRoots()/ColRoots() return the device roots.
+// A square wider than the device path (CEL_ETOOBIG: k > 512) is extended by the
+// reference call itself, rsmt2d.ComputeExtendedDataSquare with wrapper.NewConstructor,
+// exactly as data_availability_header.go:74 does: the domain stays the reference's.
 func (c *Context) ExtendSquare(shares [][]byte, codec rsmt2d.Codec) (*rsmt2d.ExtendedDataSquare, error) {
 	if n := len(shares); n == 0 || n&(n-1) != 0 {
 		return nil, fmt.Errorf("number of shares is not a power of 2: got %d", n)
 	}
-	flat, rr, cr, _, err := c.ExtendShares(shares)
+	flat, rr, cr, _, err := c.extend(shares, flagOrder|flagParity)
+	if tooBig(err) {
+		k := 1
+		for k*k < len(shares) {
+			k <<= 1
+		}
+		return rsmt2d.ComputeExtendedDataSquare(shares, codec, wrapper.NewConstructor(uint64(k)))
+	}
 	if err != nil {
 		return nil, err
 	}
@@ -148,7 +184,13 @@ func (c *Context) ExtendSquare(shares [][]byte, codec rsmt2d.Codec) (*rsmt2d.Ext
 // Codec implements rsmt2d.Codec (Encode/Decode/MaxChunks/Name/ValidateChunkSize) on
 // the device; rsmt2d's per-axis calls pay one launch each, so the square path above
 // is the fast path and this exists for API completeness (e.g. Repair from celestia-node).
+// MaxChunks is the reference's 32768^2; codewords wider than the device kernels (encode
+// n > 2048 data shards, decode n > 1024: CEL_ETOOBIG) go to the reference LeoRSCodec
+// (appconsts.DefaultCodec, global_consts.go:92), so every input the reference accepts
+// is accepted here with the reference's result.
 type Codec struct{ C *Context }
+
+var refCodec = appconsts.DefaultCodec()
 
 var _ rsmt2d.Codec = Codec{}
 
@@ -173,7 +215,9 @@ func (cd Codec) Encode(data [][]byte) ([][]byte, error) {
 	}
 	if err := cd.C.call(func() C.cel_status {
 		return C.cel_codec_encode(cd.C.ctx, (*C.uint8_t)(in), C.uint32_t(n), C.uint32_t(l), (*C.uint8_t)(out))
-	}); err != nil {
+	}); tooBig(err) {
+		return refCodec.Encode(data)
+	} else if err != nil {
 		return nil, err
 	}
 	par := unsafe.Slice((*byte)(out), n*l)
@@ -209,7 +253,9 @@ func (cd Codec) Decode(shards [][]byte) ([][]byte, error) {
 	}
 	if err := cd.C.call(func() C.cel_status {
 		return C.cel_codec_decode(cd.C.ctx, (*C.uint8_t)(buf), (*C.uint8_t)(pres), C.uint32_t(n2/2), C.uint32_t(l))
-	}); err != nil {
+	}); tooBig(err) {
+		return refCodec.Decode(shards)
+	} else if err != nil {
 		return nil, err
 	}
 	out := make([][]byte, n2)
@@ -297,6 +343,7 @@ func (c *Context) GetCommitment(eds []byte, k, start, blobShareLen, subtreeRootT
 // shares a celestia-node bad-encoding fraud proof is built from), the plain "bad root
 // input" error of preRepairSanityCheck, or rsmt2d.ErrUnrepairableDataSquare. On an
 // error present[] is left as the mask the partially repaired flat is valid under.
+// Squares wider than the device path (CEL_ETOOBIG, k > 512) are repaired by rsmt2d itself.
 func (c *Context) Repair(flat, present []byte, k int, rowRoots, colRoots [][]byte) error {
 	w := 2 * k
 	rr := make([]byte, 0, w*NmtNodeSize)
@@ -315,6 +362,26 @@ func (c *Context) Repair(flat, present []byte, k int, rowRoots, colRoots [][]byt
 			&axis, &index, (*C.uint8_t)(unsafe.Pointer(&byzShares[0])), (*C.uint8_t)(unsafe.Pointer(&byzPresent[0])))
 		return st
 	})
+	if tooBig(err) { // k > 512: rsmt2d's own Repair over the same cells
+		cells := make([][]byte, w*w)
+		for i := range cells {
+			if present[i] != 0 {
+				cells[i] = flat[i*ShareSize : (i+1)*ShareSize]
+			}
+		}
+		eds, ierr := rsmt2d.ImportExtendedDataSquare(cells, appconsts.DefaultCodec(), wrapper.NewConstructor(uint64(k)))
+		if ierr != nil {
+			return ierr
+		}
+		if rerr := eds.Repair(rowRoots, colRoots); rerr != nil {
+			return rerr
+		}
+		for i := range cells {
+			copy(flat[i*ShareSize:(i+1)*ShareSize], eds.GetCell(uint(i/w), uint(i%w)))
+			present[i] = 1
+		}
+		return nil
+	}
 	if st == C.CEL_EBYZANTINE {
 		shares := make([][]byte, w)
 		for j := range shares {

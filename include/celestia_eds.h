@@ -40,7 +40,8 @@ typedef int32_t cel_status;
 #define CEL_EINVAL 1         /* bad argument (nil pointer, zero size)                          */
 #define CEL_ENOTPOW2 2       /* "number of shares is not a power of 2: got %d" (data_availability_header.go:68) */
 #define CEL_ECHUNK 3         /* chunk size not a positive multiple of 64 (rsmt2d ValidateChunkSize) */
-#define CEL_ETOOBIG 4        /* square wider than the device path supports                     */
+#define CEL_ETOOBIG 4        /* square / codeword wider than the device path supports: the Go shim
+                                answers these calls with the reference path instead */
 #define CEL_EORDER 5         /* nmt: leaves pushed out of namespace order (nmt_wrapper_test.go:106-111) */
 #define CEL_ETOOFEW 6        /* decode: fewer than k of 2k shards present                      */
 #define CEL_EBYZANTINE 7     /* rsmt2d ErrByzantineData: axis fails re-encoding or root check  */
@@ -51,6 +52,8 @@ typedef int32_t cel_status;
 #define CEL_EPUSHPAST 12     /* "pushed past predetermined square size" (nmt_wrapper.go:95)     */
 #define CEL_EBADROOT 13      /* rsmt2d preRepairSanityCheck "bad root input": a complete axis does
                                 not match its root (a plain error, not ErrByzantineData)       */
+#define CEL_ENODATA 14       /* codec: zero-length shards (klauspost reedsolomon ErrShardNoData,
+                                "no shard data", which LeoRSCodec.Encode / Decode pass through) */
 
 /* Flags for the square entry points. */
 #define CEL_FLAG_ORDER_CHECK 0x1u   /* enforce the honest nmt push order (default in the Go path) */
@@ -219,10 +222,11 @@ cel_status cel_merkle_hash_slices(cel_ctx* ctx, const uint8_t* data, const uint6
  *   CEL_EUNREPAIRABLE ErrUnrepairableDataSquare: no progress possible.
  * On CEL_EBYZANTINE / CEL_EBADROOT present[] is the mask before the failing solve (the
  * "most-repaired square prior to the byzantine axis"); on CEL_EUNREPAIRABLE the mask of
- * the most-repaired square. Cells outside present[] are undefined. Repair checks run in
- * rsmt2d's order (sanity: row i then column i; crossword passes over all rows, then
- * all columns); rsmt2d runs its sanity checks in goroutines, so which failing axis it
- * reports first is not fixed there. */
+ * the most-repaired square. Cells outside present[] are undefined. Checks are reported
+ * in rsmt2d's order: sanity row i then column i; then solveCrossword's sweeps, row i then
+ * column i for i = 0..2k-1, each solve followed by the orthogonal axes it completes.
+ * rsmt2d runs its sanity checks in goroutines, so which failing complete axis it reports
+ * first is not fixed there. */
 cel_status cel_repair(cel_ctx* ctx, uint8_t* eds, uint8_t* present, uint32_t k,
                       uint32_t share_size, const uint8_t* row_roots, const uint8_t* col_roots,
                       int32_t* bad_axis, int32_t* bad_index, uint8_t* byz_shares,
@@ -233,6 +237,12 @@ cel_status cel_repair(cel_ctx* ctx, uint8_t* eds, uint8_t* present, uint32_t k,
 cel_status cel_dev_repair(cel_ctx* ctx, void* d_eds, uint8_t* present, uint32_t k,
                           const uint8_t* row_roots, const uint8_t* col_roots, int32_t* bad_axis,
                           int32_t* bad_index, uint8_t* byz_shares, uint8_t* byz_present);
+/* Tests only: from the next repair on ctx, an idle kernel of a pseudo-random 0..max_us
+ * microseconds (seeded by seed) goes in front of every operation the repair enqueues on
+ * either of its two streams, so the streams interleave differently; max_us = 0 turns it
+ * off. Outcomes must not change: it checks that the schedule's cross-stream dependencies
+ * are complete. */
+cel_status cel_debug_schedule_fuzz(cel_ctx* ctx, uint64_t seed, uint32_t max_us);
 
 /* ------------------------------------------------------- exported trees, proofs
  * pkg/proof (proof.go:78-202, row_proof.go, share_proof.go) and the subtree-root

@@ -218,9 +218,10 @@ int orc_extend_and_commit(const uint8_t* ods, uint32_t k, size_t share, uint8_t*
  *     and its parity half must equal Encode(data half) (else ORC_EBYZANTINE, shares =
  *     the whole axis). rsmt2d runs these checks in goroutines; this restatement fixes
  *     the order: for i in 0..W-1: row i (root, encoding), then column i.
- *  2. solveCrossword: passes over all rows, then all columns (each pass sees the square
- *     as the previous pass left it), until solved or a round makes no progress
- *     (ORC_EUNREPAIRABLE). Every incomplete axis with >= k known cells is decoded; its
+ *  2. solveCrossword: sweeps `for i in 0..W-1 { solveCrosswordRow(i); solveCrosswordCol(i) }`
+ *     (row i, then column i, each solve seeing the square as every earlier solve left it),
+ *     until solved or a sweep makes no progress (ORC_EUNREPAIRABLE).
+ *     Every incomplete axis with >= k known cells is decoded; its
  *     parity half must equal Encode(data half) and its root must match (else
  *     ORC_EBYZANTINE, shares = the axis before the solve, missing cells absent); then
  *     every orthogonal axis the solve completes (in index order) must match its root
@@ -332,9 +333,12 @@ static int solve_axis(const rep_t* R, int is_col, uint32_t idx, uint8_t* cells, 
   return 1;
 }
 
-int orc_repair(uint8_t* eds, uint8_t* present, uint32_t k, size_t share, const uint8_t* row_roots,
-               const uint8_t* col_roots, int32_t* bad_axis, int32_t* bad_index, uint8_t* byz_shares,
-               uint8_t* byz_present) {
+/* order 0: rsmt2d's sweep (row i, column i); order 1: every row, then every column, per
+ * sweep (the order of the round-1/2 restatement, kept only so a test can show that a case
+ * tells the two apart). */
+int orc_repair_order(uint8_t* eds, uint8_t* present, uint32_t k, size_t share, const uint8_t* row_roots,
+                     const uint8_t* col_roots, int32_t* bad_axis, int32_t* bad_index, uint8_t* byz_shares,
+                     uint8_t* byz_present, int order) {
   orc_init();
   rep_t R = {eds, present, k, 2 * k, share, (size_t)2 * k * share, row_roots, col_roots,
              bad_axis, bad_index, byz_shares, byz_present};
@@ -352,14 +356,15 @@ int orc_repair(uint8_t* eds, uint8_t* present, uint32_t k, size_t share, const u
   }
   while (rc == ORC_OK) {
     int progress = 0;
-    for (int is_col = 0; is_col < 2 && rc == ORC_OK; is_col++)
-      for (uint32_t i = 0; i < w; i++) {
-        uint32_t c = count_axis(&R, is_col, i);
-        if (c == w || c < k) continue;
-        int s = solve_axis(&R, is_col, i, cells, pm, ocells, opm);
-        if (s < 0) { rc = -s; break; }
-        progress = 1;
-      }
+    for (uint32_t t = 0; t < 2 * w && rc == ORC_OK; t++) {
+      const int is_col = order ? (t >= w) : (int)(t & 1);
+      const uint32_t i = order ? t % w : t >> 1;
+      uint32_t c = count_axis(&R, is_col, i);
+      if (c == w || c < k) continue;
+      int s = solve_axis(&R, is_col, i, cells, pm, ocells, opm);
+      if (s < 0) { rc = -s; break; }
+      progress = 1;
+    }
     if (rc != ORC_OK) break;
     uint64_t have = 0;
     for (size_t i = 0; i < (size_t)w * w; i++) have += present[i] ? 1 : 0;
@@ -371,4 +376,11 @@ int orc_repair(uint8_t* eds, uint8_t* present, uint32_t k, size_t share, const u
   free(pm);
   free(opm);
   return rc;
+}
+
+int orc_repair(uint8_t* eds, uint8_t* present, uint32_t k, size_t share, const uint8_t* row_roots,
+               const uint8_t* col_roots, int32_t* bad_axis, int32_t* bad_index, uint8_t* byz_shares,
+               uint8_t* byz_present) {
+  return orc_repair_order(eds, present, k, share, row_roots, col_roots, bad_axis, bad_index, byz_shares,
+                          byz_present, 0);
 }

@@ -9,10 +9,9 @@
  * The algorithm text followed is SURVEY.md Appendix A.2 / A.3 (restated from the
  * pinned dependency and verified there against mainnet block 408's data root).
  *
- * Decoding here is NOT Leopard's error-locator decoder: it is plain Gauss-Jordan
- * over the field using the generator matrix obtained by encoding unit vectors.
- * The code is MDS, so the recovered codeword is unique and any correct decoder
- * is bit-exact with klauspost Reconstruct.
+ * Decoding restates Leopard's error-locator decoder (klauspost reconstruct with
+ * recoverAll), so it matches klauspost Reconstruct also on shards that are not a
+ * codeword (byzantine squares), where decoders of the same code differ.
  */
 #include <stdlib.h>
 #include <string.h>
@@ -328,133 +327,95 @@ int orc_rs_encode(uint32_t n, size_t len, const uint8_t* data, uint8_t* parity) 
 
 /* ------------------------------------------------------------- decoding */
 
-/* Generator matrices G[i][j] = parity symbol i of encode(e_j), cached per n. */
-typedef struct {
-  uint32_t n;
-  uint16_t* g;
-} gen_cache_t;
-static gen_cache_t g_gen[16];
-
-static const uint16_t* generator(uint32_t n) {
-  int slot = __builtin_ctz(n);
-  const uint16_t* res = NULL;
-#pragma omp critical(orc_gen)
-  {
-    if (!g_gen[slot].g) {
-      const gf_t* f = field_for(n);
-      size_t slen = f->bits == 8 ? 1 : 64;
-      uint16_t* g = (uint16_t*)malloc(sizeof(uint16_t) * n * n);
-      uint8_t* buf = (uint8_t*)calloc((size_t)n * slen, 1);
-      uint8_t** w = (uint8_t**)malloc(sizeof(uint8_t*) * n);
-      int simd = g_simd;
-      g_simd = 0;
-      for (uint32_t j = 0; j < n; j++) {
-        memset(buf, 0, (size_t)n * slen);
-        buf[(size_t)j * slen] = 1; /* symbol value 1 at position 0 */
-        for (uint32_t i = 0; i < n; i++) w[i] = buf + (size_t)i * slen;
-        leo_encode_inplace(f, n, w, slen);
-        for (uint32_t i = 0; i < n; i++) {
-          uint32_t s = buf[(size_t)i * slen];
-          if (f->bits == 16) s |= (uint32_t)buf[(size_t)i * slen + 32] << 8;
-          g[(size_t)i * n + j] = (uint16_t)s;
-        }
+/* In-place Walsh-Hadamard transform mod f->mod over N points (values < mod). */
+static void fwht_mod(uint32_t* a, uint32_t N, uint32_t mod) {
+  for (uint32_t h = 1; h < N; h <<= 1)
+    for (uint32_t i = 0; i < N; i += 2 * h)
+      for (uint32_t j = i; j < i + h; j++) {
+        const uint32_t x = a[j], y = a[j + h];
+        a[j] = (x + y) % mod;
+        a[j + h] = (x + mod - y) % mod;
       }
-      g_simd = simd;
-      free(w);
-      free(buf);
-      g_gen[slot].n = n;
-      g_gen[slot].g = g;
-    }
-    res = g_gen[slot].g;
-  }
-  return res;
 }
 
-static inline uint32_t get_sym(const gf_t* f, const uint8_t* s, size_t idx) {
-  if (f->bits == 8) return s[idx];
-  size_t c = (idx / 32) * 64, j = idx % 32;
-  return (uint32_t)s[c + j] | ((uint32_t)s[c + 32 + j] << 8);
+/* x = x * exp(lm), symbol-wise (tmp: len bytes of scratch). */
+static void mul_shard(const gf_t* f, uint8_t* x, uint32_t lm, size_t len, uint8_t* tmp) {
+  memset(tmp, 0, len);
+  muladd_shard(f, tmp, x, lm, len);
+  memcpy(x, tmp, len);
 }
 
-static inline void put_sym(const gf_t* f, uint8_t* s, size_t idx, uint32_t v) {
-  if (f->bits == 8) { s[idx] = (uint8_t)v; return; }
-  size_t c = (idx / 32) * 64, j = idx % 32;
-  s[c + j] = (uint8_t)(v & 0xFF);
-  s[c + 32 + j] = (uint8_t)(v >> 8);
-}
-
+/*
+ * klauspost leopard8.go / leopard.go reconstruct with recoverAll (rsmt2d LeoRSCodec.Decode
+ * calls Reconstruct), the catid/leopard erasure decoder:
+ *   err[i]   = sum over erased e of log(i ^ e)  mod MOD   (error locator, by FWHTs)
+ *   work[i]  = present ? shard_i * exp(err[i]) : 0
+ *   work     = FFT(FormalDerivative(IFFT(work)))          (skew offset 0, N = 2n points)
+ *   shard_i  = work[i] * exp(-err[i])                     for every erased i, data and parity
+ * Leopard position p holds rsmt2d shard p ^ n (parity first, then data). Every present
+ * shard takes part, so on shards that are not a codeword the output is this formula's,
+ * not that of any other decoder (byzantine squares; no reference vector covers that
+ * case: parity unpinned there). O(N log N) shard operations per axis.
+ */
 int orc_rs_decode(uint32_t n, size_t len, uint8_t* shards, const uint8_t* present) {
   orc_init();
   if (!is_pow2(n) || n > 32768) return ORC_EINVAL;
   const gf_t* f = field_for(n);
-  if (f->bits == 16 && len % 64) return ORC_ECHUNK;
+  if (f->bits == 16) {
+    if (len % 64) return ORC_ECHUNK;
+    if (g_simd && !g_lut16) {
+#pragma omp critical(orc_lut16)
+      if (!g_lut16) build_lut16();
+    }
+  }
   uint32_t have = 0;
   for (uint32_t i = 0; i < 2 * n; i++) have += present[i] ? 1 : 0;
   if (have == 2 * n) return ORC_OK;
   if (have < n) return ORC_ETOOFEW;
-  int data_complete = 1;
-  for (uint32_t i = 0; i < n; i++) data_complete &= present[i] ? 1 : 0;
-  if (!data_complete) {
-    const uint16_t* G = generator(n);
-    uint32_t* rows = (uint32_t*)malloc(sizeof(uint32_t) * n);
-    uint32_t cnt = 0;
-    for (uint32_t i = 0; i < 2 * n && cnt < n; i++)
-      if (present[i]) rows[cnt++] = i;
-    /* A (n x n) | I -> Gauss-Jordan -> A^-1 */
-    uint16_t* a = (uint16_t*)calloc((size_t)n * 2 * n, sizeof(uint16_t));
-    for (uint32_t r = 0; r < n; r++) {
-      uint32_t p = rows[r];
-      uint16_t* row = a + (size_t)r * 2 * n;
-      if (p < n) row[p] = 1;
-      else memcpy(row, G + (size_t)(p - n) * n, sizeof(uint16_t) * n);
-      row[n + r] = 1;
-    }
-    for (uint32_t col = 0; col < n; col++) {
-      uint32_t piv = col;
-      while (piv < n && a[(size_t)piv * 2 * n + col] == 0) piv++;
-      if (piv == n) { free(a); free(rows); return ORC_EINVAL; } /* cannot happen for MDS */
-      if (piv != col)
-        for (uint32_t c = 0; c < 2 * n; c++) {
-          uint16_t t = a[(size_t)piv * 2 * n + c];
-          a[(size_t)piv * 2 * n + c] = a[(size_t)col * 2 * n + c];
-          a[(size_t)col * 2 * n + c] = t;
-        }
-      uint16_t* prow = a + (size_t)col * 2 * n;
-      uint32_t inv = gf_inv(f, prow[col]);
-      for (uint32_t c = 0; c < 2 * n; c++) prow[c] = (uint16_t)gf_mul(f, prow[c], inv);
-      for (uint32_t r = 0; r < n; r++) {
-        if (r == col) continue;
-        uint16_t* row = a + (size_t)r * 2 * n;
-        uint32_t fac = row[col];
-        if (!fac) continue;
-        for (uint32_t c = 0; c < 2 * n; c++) row[c] ^= (uint16_t)gf_mul(f, prow[c], fac);
-      }
-    }
-    /* data[i] = sum_r inv[i][r] * known[rows[r]] */
-    size_t nsym = f->bits == 8 ? len : len / 2;
-    uint8_t* out = (uint8_t*)malloc((size_t)n * len);
-    for (uint32_t i = 0; i < n; i++) {
-      const uint16_t* ir = a + (size_t)i * 2 * n + n;
-      for (size_t s = 0; s < nsym; s++) {
-        uint32_t acc = 0;
-        for (uint32_t r = 0; r < n; r++) {
-          if (!ir[r]) continue;
-          acc ^= gf_mul(f, ir[r], get_sym(f, shards + (size_t)rows[r] * len, s));
-        }
-        put_sym(f, out + (size_t)i * len, s, acc);
-      }
-    }
-    for (uint32_t i = 0; i < n; i++)
-      if (!present[i]) memcpy(shards + (size_t)i * len, out + (size_t)i * len, len);
-    free(out);
-    free(a);
-    free(rows);
+  const uint32_t N = 2 * n, mod = f->mod;
+  /* error locator: XOR convolution of the erasure flags with the log table */
+  uint32_t* err = (uint32_t*)malloc(sizeof(uint32_t) * N);
+  uint32_t* lg = (uint32_t*)malloc(sizeof(uint32_t) * N);
+  for (uint32_t p = 0; p < N; p++) {
+    err[p] = present[p ^ n] ? 0u : 1u;
+    lg[p] = f->log[p] % mod; /* log(0) = MOD == 0 */
   }
-  /* Re-encode the parity half. */
-  uint8_t* par = (uint8_t*)malloc((size_t)n * len);
-  orc_rs_encode(n, len, shards, par);
-  for (uint32_t i = 0; i < n; i++)
-    if (!present[n + i]) memcpy(shards + (size_t)(n + i) * len, par + (size_t)i * len, len);
-  free(par);
+  fwht_mod(err, N, mod);
+  fwht_mod(lg, N, mod);
+  for (uint32_t p = 0; p < N; p++) err[p] = (uint32_t)(((uint64_t)err[p] * lg[p]) % mod);
+  fwht_mod(err, N, mod);
+  /* 1/N = 2^(bits - log2 N) (2^bits == 1 mod MOD) */
+  const uint32_t inv_n = (1u << (f->bits - __builtin_ctz(N))) % mod;
+  for (uint32_t p = 0; p < N; p++) err[p] = (uint32_t)(((uint64_t)err[p] * inv_n) % mod);
+  uint8_t* buf = (uint8_t*)calloc((size_t)N + 1, len);
+  uint8_t* tmp = buf + (size_t)N * len;
+  uint8_t** w = (uint8_t**)malloc(sizeof(uint8_t*) * N);
+  for (uint32_t p = 0; p < N; p++) {
+    w[p] = buf + (size_t)p * len;
+    if (present[p ^ n]) {
+      memcpy(w[p], shards + (size_t)(p ^ n) * len, len);
+      mul_shard(f, w[p], err[p], len, tmp);
+    }
+  }
+  const uint16_t* skew = f->skew; /* skewLUT = fftSkew - 1: block b, half d -> skew[b + d - 1] */
+  for (uint32_t d = 1; d < N; d <<= 1)
+    for (uint32_t b = 0; b < N; b += 2 * d)
+      for (uint32_t j = 0; j < d; j++) ifft2(f, w[b + j], w[b + d + j], skew[b + d - 1], len);
+  for (uint32_t i = 1; i < N; i++) { /* formal derivative */
+    const uint32_t width = i & (~i + 1);
+    for (uint32_t j = 0; j < width; j++) xor_shard(w[i - width + j], w[i + j], len);
+  }
+  for (uint32_t d = N >> 1; d >= 1; d >>= 1)
+    for (uint32_t b = 0; b < N; b += 2 * d)
+      for (uint32_t j = 0; j < d; j++) fft2(f, w[b + j], w[b + d + j], skew[b + d - 1], len);
+  for (uint32_t p = 0; p < N; p++) {
+    if (present[p ^ n]) continue;
+    mul_shard(f, w[p], (mod - err[p]) % mod, len, tmp);
+    memcpy(shards + (size_t)(p ^ n) * len, w[p], len);
+  }
+  free(w);
+  free(buf);
+  free(lg);
+  free(err);
   return ORC_OK;
 }

@@ -102,6 +102,11 @@ int orc_extend_and_commit(const uint8_t* ods, uint32_t k, size_t share, uint8_t*
 int orc_repair(uint8_t* eds, uint8_t* present, uint32_t k, size_t share,
                const uint8_t* row_roots, const uint8_t* col_roots, int32_t* bad_axis,
                int32_t* bad_index, uint8_t* byz_shares, uint8_t* byz_present);
+/* Same, with the sweep order as a parameter: 0 = rsmt2d's (row i, then column i), 1 = all
+ * rows, then all columns (test use only: shows that a case distinguishes the orders). */
+int orc_repair_order(uint8_t* eds, uint8_t* present, uint32_t k, size_t share,
+                     const uint8_t* row_roots, const uint8_t* col_roots, int32_t* bad_axis,
+                     int32_t* bad_index, uint8_t* byz_shares, uint8_t* byz_present, int order);
 
 #ifdef __cplusplus
 }

@@ -49,6 +49,7 @@ def lib():
         l.orc_dah_hash.argtypes = [P, P, u32, P]
         l.orc_extend_and_commit.argtypes = [P, u32, sz, P, P, P, P]
         l.orc_repair.argtypes = [P, P, u32, sz, P, P, P, P, P, P]
+        l.orc_repair_order.argtypes = [P, P, u32, sz, P, P, P, P, P, P, i32]
         l.orc_init()
         _lib = l
     return _lib
@@ -165,17 +166,19 @@ def extend_and_commit(ods: np.ndarray, want_eds=True):
     return eds, rr, cr, dah.tobytes()
 
 
-def repair(eds: np.ndarray, present: np.ndarray, row_roots, col_roots, want_shares=False):
+def repair(eds: np.ndarray, present: np.ndarray, row_roots, col_roots, want_shares=False, order=0):
     """rsmt2d Repair restatement (eds.c). Returns (rc, eds, present, (axis, index)), plus
-    (byz_shares (W, share), byz_present (W,)) when want_shares."""
+    (byz_shares (W, share), byz_present (W,)) when want_shares. order 0 = rsmt2d's sweep
+    (row i, then column i); 1 = all rows, then all columns (tests only)."""
     eds = np.ascontiguousarray(eds, dtype=np.uint8).copy()
     present = np.ascontiguousarray(present, dtype=np.uint8).copy()
     w, _, share = eds.shape
     ba, bi = ctypes.c_int32(-1), ctypes.c_int32(-1)
     bs = np.zeros((w, share), np.uint8)
     bp = np.zeros(w, np.uint8)
-    rc = lib().orc_repair(_p(eds), _p(present), w // 2, share, _p(np.ascontiguousarray(row_roots)),
-                          _p(np.ascontiguousarray(col_roots)), ctypes.byref(ba), ctypes.byref(bi), _p(bs), _p(bp))
+    rc = lib().orc_repair_order(_p(eds), _p(present), w // 2, share, _p(np.ascontiguousarray(row_roots)),
+                                _p(np.ascontiguousarray(col_roots)), ctypes.byref(ba), ctypes.byref(bi), _p(bs),
+                                _p(bp), int(order))
     if want_shares:
         return rc, eds, present, (ba.value, bi.value), (bs, bp)
     return rc, eds, present, (ba.value, bi.value)

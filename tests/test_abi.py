@@ -47,6 +47,19 @@ def test_device_independent_entry_points():
     assert lib.cel_dev_workspace_size(128, 1) > 0
 
 
+def test_status_codes_match_header():
+    """Every CEL_E* code of the header equals the binding's constant: the Go shim keys its
+    fallback to the reference path on CEL_ETOOBIG and its errors on the rest, so the
+    numbers are part of the ABI (strerror texts included)."""
+    import celestia_eds._lib as L
+    codes = dict(re.findall(r"^#define CEL_(OK|E[A-Z]+) (\d+)", open(HEADER).read(), re.M))
+    assert {k: int(v) for k, v in codes.items()} == {k: getattr(L, k) for k in codes}
+    assert int(codes["ETOOBIG"]) == 4 and int(codes["ENODATA"]) == 14
+    lib = L.load()
+    assert lib.cel_strerror(L.ENODATA).decode() == "no shard data"
+    assert lib.cel_strerror(L.ETOOBIG).decode() == "square too large for the device path"
+
+
 def test_gfx950_code_object():
     """The library carries a gfx950 code object in its HIP fat binary."""
     data = open(LIB, "rb").read()

@@ -73,8 +73,11 @@ def test_decode_too_few(ctx):
 
 
 def test_device_limits(ctx):
-    """The device codec's shard-count limits fail loudly (ETOOBIG), never fall back:
-    encode takes n <= 2048 data shards (the LDS image), decode n <= 1024."""
+    """The device codec's shard-count limits fail loudly with exactly ETOOBIG, the status
+    the Go shim keys its fallback to the reference LeoRSCodec on:
+    encode takes n <= 2048 data shards (the LDS image), decode n <= 1024; a square wider
+    than k = 512 is ETOOBIG too (ExtendSquare's fallback to rsmt2d). Zero-length shards
+    are klauspost's ErrShardNoData ("no shard data")."""
     from celestia_eds import CelError, _lib
     from celestia_eds.rsmt2d import LeoRSCodec
     codec = LeoRSCodec(ctx)
@@ -84,3 +87,14 @@ def test_device_limits(ctx):
     with pytest.raises(CelError) as ei:
         codec.Decode([bytes(64)] * 2048 + [None] * 2048)
     assert ei.value.status == _lib.ETOOBIG
+    with pytest.raises(CelError) as ei:
+        codec.Encode([b""] * 4)
+    assert ei.value.status == _lib.ENODATA and "no shard data" in str(ei.value)
+    with pytest.raises(CelError) as ei:
+        codec.Decode([b""] * 4 + [None] * 4)
+    assert ei.value.status == _lib.ENODATA
+    import ctypes
+    k = 1024  # status only: the size check precedes any copy (small stand-in buffers)
+    z = np.zeros(64, np.uint8).ctypes.data_as(ctypes.c_void_p)
+    st = ctx.lib.cel_extend_shares(ctx.handle, z, k * k, 512, None, z, z, z, 0)
+    assert st == _lib.ETOOBIG

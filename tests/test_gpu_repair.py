@@ -52,6 +52,7 @@ def test_random_025_unrepairable(ctx, oracle):
 
 
 def test_corrupt_cell_byzantine(ctx, oracle):
+    from celestia_eds import _lib
     from celestia_eds.rsmt2d import ErrByzantineData
     k = 16
     eds, rr, cr = setup(oracle, k)
@@ -62,11 +63,13 @@ def test_corrupt_cell_byzantine(ctx, oracle):
     present[9, 1] = 0
     bad = eds.copy()
     bad[0, 1, 200] ^= 0x40
+    st, axis, bs, bp = _assert_same_outcome(ctx, oracle, bad, present, rr, cr)
+    assert st == _lib.EBYZANTINE
     from celestia_eds.rsmt2d import ExtendedDataSquare
-    sq = ExtendedDataSquare(bad, ctx=ctx)
+    sq = ExtendedDataSquare(np.where(present[..., None] == 1, bad, 0).astype(np.uint8), ctx=ctx)
     with pytest.raises(ErrByzantineData) as ei:
         sq.Repair(rr, cr, present=present)
-    assert ei.value.Axis in (0, 1) and ei.value.Index >= 0
+    assert (ei.value.Axis, ei.value.Index) == axis
 
 
 def test_gf16_repair_k256(ctx, oracle):
@@ -375,3 +378,131 @@ def test_dev_repair_random_masks(ctx, oracle, k):
                 assert st == _lib.OK and np.array_equal(cells, eds), (seed, p)
             else:
                 assert st == _lib.EUNREPAIRABLE, (seed, p, st)
+
+
+@pytest.mark.parametrize("k", [8, 32, 256])
+def test_missing_cells_hold_garbage(ctx, oracle, k):
+    """The Repair ABI lets missing cells hold anything: random bytes there must not reach
+    the decoders (k = 8 and 256: the LDS decoder, which zeroes erased points at its load;
+    k = 32: the in-square register decoder, whose erased points scale by zero)."""
+    from celestia_eds import _lib
+    eds, rr, cr = setup(oracle, k, seed=5)
+    w = 2 * k
+    rng = np.random.default_rng(k)
+    present = (rng.random((w, w)) < 0.6).astype(np.uint8)
+    junk = np.where(present[..., None] == 1, eds, rng.integers(0, 256, eds.shape, dtype=np.uint8))
+    import ctypes
+    from hipmem import DeviceBuffer
+    d = DeviceBuffer(junk.nbytes)
+    d.upload(np.ascontiguousarray(junk))
+    pres = present.copy()
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    rra, cra = _stack(rr), _stack(cr)
+    st = ctx.lib.cel_dev_repair(ctx.handle, d.ptr, P(pres), k, P(rra), P(cra), None, None, None, None)
+    assert st == _lib.OK and np.array_equal(d.download(eds.shape), eds)
+
+
+def test_codec_decode_ignores_erased_bytes(ctx, oracle):
+    """cel_codec_decode / cel_dev_decode: erased shards' bytes are not inputs (n = 8 and
+    1024: the LDS decoder; n = 64: the register decoder)."""
+    import ctypes
+    from celestia_eds import _lib
+    for n in (8, 64, 1024):
+        rng = np.random.default_rng(n)
+        data = rng.integers(0, 256, (n, 128), dtype=np.uint8)
+        cw = np.concatenate([data, oracle.rs_encode(data)])
+        present = np.ones(2 * n, np.uint8)
+        present[rng.choice(2 * n, n, replace=False)] = 0
+        buf = np.where(present[:, None] == 1, cw, rng.integers(0, 256, cw.shape, dtype=np.uint8)).astype(np.uint8)
+        P = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+        assert ctx.lib.cel_codec_decode(ctx.handle, P(buf), P(present), n, 128) == _lib.OK
+        assert np.array_equal(buf, cw), n
+
+
+def test_decode_inconsistent_shards_matches_oracle(ctx, oracle):
+    """Shards that are not a codeword (byzantine input): the device decoders compute
+    Leopard's error-locator formula over every present shard, erased data and parity alike
+    (klauspost reconstruct, recoverAll), like the oracle's restatement; Gauss-Jordan over
+    any k of them would differ. Parity unpinned (no reference vector decodes such input)."""
+    import ctypes
+    from celestia_eds import _lib
+    for n in (8, 16, 32, 128, 256, 512):
+        rng = np.random.default_rng(100 + n)
+        data = rng.integers(0, 256, (n, 128), dtype=np.uint8)
+        cw = np.concatenate([data, oracle.rs_encode(data)])
+        present = np.ones(2 * n, np.uint8)
+        present[rng.choice(2 * n, n // 2, replace=False)] = 0
+        bad = cw.copy()
+        for j in rng.choice(np.flatnonzero(present), 3, replace=False):
+            bad[j, rng.integers(0, 128)] ^= 0x3C
+        bad[present == 0] = 0
+        exp = oracle.rs_decode(bad, present)
+        buf = bad.copy()
+        P = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+        assert ctx.lib.cel_codec_decode(ctx.handle, P(buf), P(present), n, 128) == _lib.OK
+        assert np.array_equal(buf, exp), n
+        assert not np.array_equal(buf, cw)
+
+
+# --- rsmt2d's sweep order (row i, then column i) decides which byzantine axis is reported
+
+
+def _byz_case(oracle, k, seed):
+    """A random mask (p = 0.5 / 0.6 / 0.7 by seed) with two corrupted present cells."""
+    eds, rr, cr = setup(oracle, k, seed=3)
+    w = 2 * k
+    rng = np.random.default_rng(seed)
+    p = [0.5, 0.6, 0.7][seed % 3]
+    present = (rng.random((w, w)) < p).astype(np.uint8)
+    bad = eds.copy()
+    for _ in range(2):
+        r, c = rng.integers(0, w, 2)
+        present[r, c] = 1
+        bad[r, c, rng.integers(0, 512)] ^= 0x5A
+    return bad, present, rr, cr
+
+
+@pytest.mark.parametrize("k,seed", [(8, 0), (32, 0), (32, 2), (128, 0)])
+def test_sweep_order_byzantine(ctx, oracle, k, seed):
+    """Cases where rsmt2d's sweep (row i, then column i) reports a different byzantine axis
+    than all-rows-then-all-columns passes would: the device (pass-parallel schedule, then
+    the exact replay in rsmt2d's order) reports the oracle's sweep-order outcome, Shares
+    and mask included. k = 8: gather -> LDS decoder; k >= 16: the in-square decoder."""
+    from celestia_eds import _lib
+    bad, present, rr, cr = _byz_case(oracle, k, seed)
+    damaged = np.where(present[..., None] == 1, bad, 0).astype(np.uint8)
+    o_sweep = oracle.repair(damaged, present, _stack(rr), _stack(cr), order=0)
+    o_pass = oracle.repair(damaged, present, _stack(rr), _stack(cr), order=1)
+    assert o_sweep[0] == o_pass[0] == _lib.EBYZANTINE
+    assert o_sweep[3] != o_pass[3]  # the case tells the orders apart
+    st, axis, _, _ = _assert_same_outcome(ctx, oracle, bad, present, rr, cr)
+    assert axis == o_sweep[3]
+
+
+@pytest.mark.parametrize("k", [32, 128, 256])
+def test_repair_schedule_fuzz(ctx, oracle, k):
+    """The repair's two streams with a random idle kernel (0..max us) in front of every
+    operation either stream enqueues (cel_debug_schedule_fuzz), over several seeds: any
+    missing cross-stream dependency (a check reading a buffer the chain is still writing,
+    a decode reusing a buffer a check still reads) would change an outcome. Multi-pass
+    solvable and stuck masks, and a byzantine square (exact replay)."""
+    from celestia_eds import _lib
+    eds, rr, cr = setup(oracle, k, seed=3)
+    w = 2 * k
+    masks = [(np.random.default_rng(s).random((w, w)) < p).astype(np.uint8)
+             for s, p in ((1, 0.44), (2, 0.46), (25, 0.44))]
+    try:
+        for fseed in range(3):
+            assert ctx.lib.cel_debug_schedule_fuzz(ctx.handle, 1000 + fseed, 60) == _lib.OK
+            for present in masks:
+                _, ok = _crossword_passes(present, k)
+                st, cells, _ = _dev_repair(ctx, eds, present, rr, cr)
+                if ok:
+                    assert st == _lib.OK and np.array_equal(cells, eds), fseed
+                else:
+                    assert st == _lib.EUNREPAIRABLE, (fseed, st)
+            if k <= 128:
+                bad, present, brr, bcr = _byz_case(oracle, k, 0)
+                _assert_same_outcome(ctx, oracle, bad, present, brr, bcr)
+    finally:
+        ctx.lib.cel_debug_schedule_fuzz(ctx.handle, 0, 0)

@@ -100,6 +100,88 @@ def test_decode_round_trip(oracle, n):
         assert np.array_equal(oracle.rs_decode(sh, present), cw)
 
 
+def _leopard_decode_py(oracle, shards, present):
+    """Pure-Python catid/leopard erasure decoder over GF(2^8) (klauspost leopard8.go
+    reconstruct with recoverAll), with the error locator as the direct sum
+    err[i] = sum_{e erased} log(i ^ e) instead of the oracle's FWHTs, and radix-2 layers
+    instead of its loops: an independent statement of the same formula."""
+    lib = oracle.lib()
+    exp = [lib.orc_gf_exp(8, i) for i in range(256)]
+    log = [lib.orc_gf_log(8, i) for i in range(256)]
+    skew = [lib.orc_gf_skew(8, i) for i in range(255)]
+    mod = 255
+
+    def mul(a, lm):  # mulLog with klauspost's partial reduction
+        if a == 0:
+            return 0
+        s = log[a] + lm
+        return exp[(s + (s >> 8)) & mod]
+
+    n2, ln = shards.shape
+    n = n2 // 2
+    er = [p for p in range(n2) if not present[p ^ n]]
+    err = [sum(log[i ^ e] % mod for e in er) % mod for i in range(n2)]
+    w = [[mul(int(b), err[p]) for b in shards[p ^ n]] if present[p ^ n] else [0] * ln for p in range(n2)]
+    d = 1
+    while d < n2:
+        for b in range(0, n2, 2 * d):
+            lm = skew[b + d - 1]
+            for j in range(d):
+                x, y = w[b + j], w[b + d + j]
+                y = [a ^ c for a, c in zip(y, x)]
+                if lm != mod:
+                    x = [a ^ mul(c, lm) for a, c in zip(x, y)]
+                w[b + j], w[b + d + j] = x, y
+        d *= 2
+    old = [row[:] for row in w]
+    for x in range(n2):
+        t = 1
+        while t < n2:
+            if not x & t and x + t < n2:
+                w[x] = [a ^ c for a, c in zip(w[x], old[x + t])]
+            t *= 2
+    d = n2 // 2
+    while d >= 1:
+        for b in range(0, n2, 2 * d):
+            lm = skew[b + d - 1]
+            for j in range(d):
+                x, y = w[b + j], w[b + d + j]
+                if lm != mod:
+                    x = [a ^ mul(c, lm) for a, c in zip(x, y)]
+                y = [a ^ c for a, c in zip(y, x)]
+                w[b + j], w[b + d + j] = x, y
+        d //= 2
+    out = shards.copy()
+    for p in er:
+        out[p ^ n] = [mul(v, (mod - err[p]) % mod) for v in w[p]]
+    return out
+
+
+@pytest.mark.parametrize("n", [1, 2, 4, 8, 16])
+def test_decode_formula_on_inconsistent_shards(oracle, n):
+    """The oracle's decoder is Leopard's formula (not any decoder of the code): on shards
+    that are not a codeword it equals an independent pure-Python statement of the
+    formula, and differs from the codeword a subset decode would give."""
+    rng = np.random.default_rng(40 + n)
+    data = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    cw = np.concatenate([data, oracle.rs_encode(data)])
+    for simd in (False, True):
+        oracle.set_simd(simd)
+        for trial in range(3):
+            present = np.ones(2 * n, np.uint8)
+            present[rng.choice(2 * n, max(1, n // 2), replace=False)] = 0
+            bad = cw.copy()
+            j = rng.choice(np.flatnonzero(present))
+            bad[j, rng.integers(0, 16)] ^= 0x81
+            bad[present == 0] = 0
+            got = oracle.rs_decode(bad, present)
+            assert np.array_equal(got, _leopard_decode_py(oracle, bad, present))
+            good = cw.copy()
+            good[present == 0] = 0
+            assert np.array_equal(oracle.rs_decode(good, present), cw)
+    oracle.set_simd(False)
+
+
 def test_decode_too_few(oracle):
     n = 4
     sh = np.zeros((2 * n, 64), np.uint8)

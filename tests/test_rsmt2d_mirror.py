@@ -41,9 +41,12 @@ def test_custom_tree_constructor_is_honoured():
 def test_default_wrapper_constructor_is_recognised():
     from celestia_eds import wrapper
     from celestia_eds.rsmt2d import _default_constructor
-    assert _default_constructor(None)
-    assert _default_constructor(wrapper.NewConstructor(4))
-    assert not _default_constructor(CountingTree)
+    assert _default_constructor(None, 8)
+    assert _default_constructor(wrapper.NewConstructor(4), 8)
+    assert not _default_constructor(CountingTree, 8)
+    # a wrapper constructor for another square size is the caller's own trees
+    assert not _default_constructor(wrapper.NewConstructor(2), 8)
+    assert not _default_constructor(wrapper.NewConstructor(8), 8)
 
 
 def test_foreign_codec_is_refused():
