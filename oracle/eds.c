@@ -17,6 +17,9 @@
  */
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 #include "oracle.h"
 #include "oracle_internal.h"
 
@@ -26,21 +29,35 @@ static const uint8_t kParityNs[ORC_NS] = {
 
 /* ------------------------------------------------------------------- NMT */
 
-/* HashLeaf: ns || ns || SHA256(0x00 || ns || data) where ndata = ns || data. */
+/* HashLeaf: ns || ns || SHA256(0x00 || ns || data) where ndata = ns || data. The
+ * message (542 B for a share) is laid out once with its padding and hashed in one
+ * block-function call (9 blocks), like Go crypto/sha256's block loop over a Write. */
 static void nmt_leaf(const uint8_t* ns, const uint8_t* data, size_t len, uint8_t out[ORC_NODE]) {
-  static const uint8_t zero = 0x00;
   uint8_t d[32];
-  sha256_3(&zero, 1, ns, ORC_NS, data, len, d);
+  if (len <= 512) {
+    uint8_t msg[640];
+    msg[0] = 0x00;
+    memcpy(msg + 1, ns, ORC_NS);
+    memcpy(msg + 1 + ORC_NS, data, len);
+    sha256_blocks(msg, sha256_pad(msg, 1 + ORC_NS + len), d);
+  } else {
+    static const uint8_t zero = 0x00;
+    sha256_3(&zero, 1, ns, ORC_NS, data, len, d);
+  }
   memcpy(out, ns, ORC_NS);
   memcpy(out + ORC_NS, ns, ORC_NS);
   memcpy(out + 2 * ORC_NS, d, 32);
 }
 
-/* HashNode with IgnoreMaxNamespace: min = L.min; max = (R.min == MAX) ? L.max : R.max. */
+/* HashNode with IgnoreMaxNamespace: min = L.min; max = (R.min == MAX) ? L.max : R.max.
+ * 0x01 || L || R = 181 B: three padded blocks, one block-function call. */
 static void nmt_node(const uint8_t* l, const uint8_t* r, uint8_t out[ORC_NODE]) {
-  static const uint8_t one = 0x01;
   uint8_t d[32];
-  sha256_3(&one, 1, l, ORC_NODE, r, ORC_NODE, d);
+  uint8_t msg[192];
+  msg[0] = 0x01;
+  memcpy(msg + 1, l, ORC_NODE);
+  memcpy(msg + 1 + ORC_NODE, r, ORC_NODE);
+  sha256_blocks(msg, sha256_pad(msg, 1 + 2 * ORC_NODE), d);
   uint8_t res[ORC_NODE];
   memcpy(res, l, ORC_NS);
   if (memcmp(r, kParityNs, ORC_NS) == 0) memcpy(res + ORC_NS, l + ORC_NS, ORC_NS);
@@ -383,4 +400,60 @@ int orc_repair(uint8_t* eds, uint8_t* present, uint32_t k, size_t share, const u
                uint8_t* byz_present) {
   return orc_repair_order(eds, present, k, share, row_roots, col_roots, bad_axis, bad_index, byz_shares,
                           byz_present, 0);
+}
+
+/* ------------------------------------------------------- CPU baseline (bench) */
+/*
+ * Throughput form of the reference's CPU path on a multi-core host: independent squares
+ * (or repairs) on independent threads, each single-threaded inside with buffers reused
+ * across its squares, the way a node extends one block per goroutine set. Not a checker.
+ */
+int orc_extend_commit_many(const uint8_t* ods, uint32_t n, uint32_t k, size_t share, uint8_t* dah_out) {
+  orc_init();
+  const size_t ods_b = (size_t)k * k * share, eds_b = 4 * ods_b;
+  int rc = ORC_OK;
+#ifdef _OPENMP
+  const int levels = omp_get_max_active_levels();
+  omp_set_max_active_levels(1);
+#endif
+#pragma omp parallel reduction(| : rc)
+  {
+    uint8_t* eds = (uint8_t*)malloc(eds_b);
+    uint8_t* rr = (uint8_t*)malloc((size_t)2 * k * ORC_NODE);
+    uint8_t* cr = (uint8_t*)malloc((size_t)2 * k * ORC_NODE);
+#pragma omp for schedule(dynamic, 1)
+    for (int64_t i = 0; i < (int64_t)n; i++) {
+      int r = orc_extend(ods + (size_t)i * ods_b, k, share, eds);
+      if (r == ORC_OK) r = orc_roots(eds, k, share, rr, cr, 1, NULL);
+      if (r == ORC_OK) orc_dah_hash(rr, cr, 2 * k, dah_out + (size_t)i * 32);
+      rc |= r;
+    }
+    free(eds);
+    free(rr);
+    free(cr);
+  }
+#ifdef _OPENMP
+  omp_set_max_active_levels(levels);
+#endif
+  return rc;
+}
+
+int orc_repair_many(const uint8_t* eds, const uint8_t* present, uint32_t k, size_t share, const uint8_t* row_roots,
+                    const uint8_t* col_roots, uint32_t n, int32_t* status_out) {
+  orc_init();
+  const size_t cells = (size_t)4 * k * k, eds_b = cells * share;
+#pragma omp parallel
+  {
+    uint8_t* e = (uint8_t*)malloc(eds_b);
+    uint8_t* p = (uint8_t*)malloc(cells);
+#pragma omp for schedule(dynamic, 1)
+    for (int64_t i = 0; i < (int64_t)n; i++) {
+      memcpy(e, eds, eds_b);
+      memcpy(p, present, cells);
+      status_out[i] = orc_repair(e, p, k, share, row_roots, col_roots, NULL, NULL, NULL, NULL);
+    }
+    free(e);
+    free(p);
+  }
+  return ORC_OK;
 }

@@ -96,7 +96,24 @@ static void gf_build(gf_t* f, int bits, uint32_t poly, const uint16_t* cantor) {
 
 /* Nibble product tables for the SIMD (baseline) path. */
 static uint8_t (*g_lut8)[2][16];   /* [256 log][lo/hi][16] */
+/* GF2P8AFFINEQB matrices of y -> y * exp(lm): a product by a constant is GF(2)-linear on
+ * the 8 bits of y in any representation (Leopard's Cantor basis included), so one affine
+ * instruction multiplies 64 bytes (klauspost's GFNI kernels do the same). */
+static uint64_t g_aff8[256];
+static int g_gfni = 0;
 static uint8_t (*g_lut16)[8][16];  /* [65536 log][q*2 + outbyte][16] */
+
+static void build_aff8(void) {
+  for (uint32_t lm = 0; lm < 256; lm++) {
+    uint64_t a = 0;
+    for (int i = 0; i < 8; i++) { /* row of output bit i lives in byte 7 - i */
+      uint32_t row = 0;
+      for (int b = 0; b < 8; b++) row |= ((gf_mul_log(&g_gf8, 1u << b, lm) >> i) & 1u) << b;
+      a |= (uint64_t)row << (8 * (7 - i));
+    }
+    g_aff8[lm] = a;
+  }
+}
 
 static void build_lut8(void) {
   g_lut8 = malloc(sizeof(*g_lut8) * 256);
@@ -125,6 +142,11 @@ void orc_init(void) {
   gf_build(&g_gf8, 8, 0x11D, kCantor8);
   gf_build(&g_gf16, 16, 0x1002D, kCantor16);
   build_lut8();
+  build_aff8();
+#if defined(__x86_64__)
+  __builtin_cpu_init();
+  g_gfni = __builtin_cpu_supports("gfni") && __builtin_cpu_supports("avx512bw") && __builtin_cpu_supports("avx512f");
+#endif
   g_inited = 1;
 }
 
@@ -195,6 +217,17 @@ __attribute__((target("avx2"))) static void muladd8_avx2(uint8_t* x, const uint8
   for (; i < len; i++) x[i] ^= (uint8_t)gf_mul_log(&g_gf8, y[i], lm);
 }
 
+__attribute__((target("avx512f,avx512bw,gfni"))) static void muladd8_gfni(uint8_t* x, const uint8_t* y,
+                                                                          uint32_t lm, size_t len) {
+  const __m512i a = _mm512_set1_epi64((long long)g_aff8[lm]);
+  size_t i = 0;
+  for (; i + 64 <= len; i += 64) {
+    const __m512i p = _mm512_gf2p8affine_epi64_epi8(_mm512_loadu_si512((const void*)(y + i)), a, 0);
+    _mm512_storeu_si512((void*)(x + i), _mm512_xor_si512(_mm512_loadu_si512((const void*)(x + i)), p));
+  }
+  for (; i < len; i++) x[i] ^= (uint8_t)gf_mul_log(&g_gf8, y[i], lm);
+}
+
 __attribute__((target("avx2"))) static void muladd16_avx2(uint8_t* x, const uint8_t* y,
                                                            uint32_t lm, size_t len) {
   const uint8_t (*t)[16] = g_lut16[lm];
@@ -227,6 +260,7 @@ __attribute__((target("avx2"))) static void muladd16_avx2(uint8_t* x, const uint
 static void muladd_shard(const gf_t* f, uint8_t* x, const uint8_t* y, uint32_t lm, size_t len) {
   if (f->bits == 8) {
 #if defined(__x86_64__)
+    if (g_simd && g_gfni) { muladd8_gfni(x, y, lm, len); return; }
     if (g_simd) { muladd8_avx2(x, y, lm, len); return; }
 #endif
     for (size_t i = 0; i < len; i++) x[i] ^= (uint8_t)gf_mul_log(f, y[i], lm);
@@ -255,9 +289,69 @@ static void fft2(const gf_t* f, uint8_t* x, uint8_t* y, uint32_t lm, size_t len)
   xor_shard(y, x, len);
 }
 
+#if defined(__x86_64__)
+/* Radix-4 butterflies of one 64-byte column of four shards at distance d, GFNI + AVX-512
+ * (klauspost's ifftDIT48 / fftDIT48 GFNI kernels: two layers per pass over memory).
+ * A zero matrix stands for log_m == MOD (the butterfly's multiply is skipped). */
+static inline uint64_t aff8(uint32_t lm) { return lm == 255u ? 0ull : g_aff8[lm]; }
+
+__attribute__((target("avx512f,avx512bw,gfni"))) static void ifft4_gfni(uint8_t** w, uint32_t i, uint32_t d,
+                                                                        uint32_t l01, uint32_t l23, uint32_t l02,
+                                                                        size_t len) {
+  const __m512i a01 = _mm512_set1_epi64((long long)aff8(l01)), a23 = _mm512_set1_epi64((long long)aff8(l23)),
+                a02 = _mm512_set1_epi64((long long)aff8(l02));
+  uint8_t *p0 = w[i], *p1 = w[i + d], *p2 = w[i + 2 * d], *p3 = w[i + 3 * d];
+  for (size_t c = 0; c < len; c += 64) {
+    __m512i v0 = _mm512_loadu_si512(p0 + c), v1 = _mm512_loadu_si512(p1 + c);
+    __m512i v2 = _mm512_loadu_si512(p2 + c), v3 = _mm512_loadu_si512(p3 + c);
+    v1 = _mm512_xor_si512(v1, v0);
+    v0 = _mm512_xor_si512(v0, _mm512_gf2p8affine_epi64_epi8(v1, a01, 0));
+    v3 = _mm512_xor_si512(v3, v2);
+    v2 = _mm512_xor_si512(v2, _mm512_gf2p8affine_epi64_epi8(v3, a23, 0));
+    v2 = _mm512_xor_si512(v2, v0);
+    v0 = _mm512_xor_si512(v0, _mm512_gf2p8affine_epi64_epi8(v2, a02, 0));
+    v3 = _mm512_xor_si512(v3, v1);
+    v1 = _mm512_xor_si512(v1, _mm512_gf2p8affine_epi64_epi8(v3, a02, 0));
+    _mm512_storeu_si512(p0 + c, v0);
+    _mm512_storeu_si512(p1 + c, v1);
+    _mm512_storeu_si512(p2 + c, v2);
+    _mm512_storeu_si512(p3 + c, v3);
+  }
+}
+
+__attribute__((target("avx512f,avx512bw,gfni"))) static void fft4_gfni(uint8_t** w, uint32_t i, uint32_t d,
+                                                                       uint32_t l01, uint32_t l23, uint32_t l02,
+                                                                       size_t len) {
+  const __m512i a01 = _mm512_set1_epi64((long long)aff8(l01)), a23 = _mm512_set1_epi64((long long)aff8(l23)),
+                a02 = _mm512_set1_epi64((long long)aff8(l02));
+  uint8_t *p0 = w[i], *p1 = w[i + d], *p2 = w[i + 2 * d], *p3 = w[i + 3 * d];
+  for (size_t c = 0; c < len; c += 64) {
+    __m512i v0 = _mm512_loadu_si512(p0 + c), v1 = _mm512_loadu_si512(p1 + c);
+    __m512i v2 = _mm512_loadu_si512(p2 + c), v3 = _mm512_loadu_si512(p3 + c);
+    v0 = _mm512_xor_si512(v0, _mm512_gf2p8affine_epi64_epi8(v2, a02, 0));
+    v2 = _mm512_xor_si512(v2, v0);
+    v1 = _mm512_xor_si512(v1, _mm512_gf2p8affine_epi64_epi8(v3, a02, 0));
+    v3 = _mm512_xor_si512(v3, v1);
+    v0 = _mm512_xor_si512(v0, _mm512_gf2p8affine_epi64_epi8(v1, a01, 0));
+    v1 = _mm512_xor_si512(v1, v0);
+    v2 = _mm512_xor_si512(v2, _mm512_gf2p8affine_epi64_epi8(v3, a23, 0));
+    v3 = _mm512_xor_si512(v3, v2);
+    _mm512_storeu_si512(p0 + c, v0);
+    _mm512_storeu_si512(p1 + c, v1);
+    _mm512_storeu_si512(p2 + c, v2);
+    _mm512_storeu_si512(p3 + c, v3);
+  }
+}
+#endif
+
 /* In-place Leopard encode: work[0..m) holds the m data shards on entry and the m
  * parity shards on exit (klauspost ifftDITEncoder + fftDIT with mtrunc = m). */
 void leo_encode_inplace(const gf_t* f, uint32_t m, uint8_t** w, size_t len) {
+#if defined(__x86_64__)
+  const int fused = f->bits == 8 && g_simd && g_gfni && len % 64 == 0;
+#else
+  const int fused = 0;
+#endif
   const uint16_t* skew = f->skew;
   const uint16_t* sk = skew + (m - 1); /* skewLUT = fftSkew[m-1:] */
   /* IFFT, decimation in time, two layers at a time. */
@@ -266,6 +360,12 @@ void leo_encode_inplace(const gf_t* f, uint32_t m, uint8_t** w, size_t len) {
     for (uint32_t r = 0; r < m; r += dist4) {
       uint32_t ie = r + dist;
       uint32_t l01 = sk[ie], l02 = sk[ie + dist], l23 = sk[ie + 2 * dist];
+#if defined(__x86_64__)
+      if (fused) {
+        for (uint32_t i = r; i < ie; i++) ifft4_gfni(w, i, dist, l01, l23, l02, len);
+        continue;
+      }
+#endif
       for (uint32_t i = r; i < ie; i++) {
         ifft2(f, w[i], w[i + dist], l01, len);
         ifft2(f, w[i + 2 * dist], w[i + 3 * dist], l23, len);
@@ -287,6 +387,12 @@ void leo_encode_inplace(const gf_t* f, uint32_t m, uint8_t** w, size_t len) {
     for (uint32_t r = 0; r < m; r += dist4) {
       uint32_t ie = r + dist;
       uint32_t l01 = skew[ie - 1], l02 = skew[ie + dist - 1], l23 = skew[ie + 2 * dist - 1];
+#if defined(__x86_64__)
+      if (fused) {
+        for (uint32_t i = r; i < ie; i++) fft4_gfni(w, i, dist, l01, l23, l02, len);
+        continue;
+      }
+#endif
       for (uint32_t i = r; i < ie; i++) {
         fft2(f, w[i], w[i + 2 * dist], l02, len);
         fft2(f, w[i + dist], w[i + 3 * dist], l02, len);

@@ -108,6 +108,13 @@ int orc_repair_order(uint8_t* eds, uint8_t* present, uint32_t k, size_t share,
                      const uint8_t* row_roots, const uint8_t* col_roots, int32_t* bad_axis,
                      int32_t* bad_index, uint8_t* byz_shares, uint8_t* byz_present, int order);
 
+/* CPU baseline (bench.py only): n independent squares (ods: n*k*k*share) extended,
+ * committed and hashed on parallel threads, single-threaded each -> dah_out (n*32); and
+ * n independent repairs of copies of one damaged square (status_out: n codes). */
+int orc_extend_commit_many(const uint8_t* ods, uint32_t n, uint32_t k, size_t share, uint8_t* dah_out);
+int orc_repair_many(const uint8_t* eds, const uint8_t* present, uint32_t k, size_t share,
+                    const uint8_t* row_roots, const uint8_t* col_roots, uint32_t n, int32_t* status_out);
+
 #ifdef __cplusplus
 }
 #endif

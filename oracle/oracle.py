@@ -50,6 +50,8 @@ def lib():
         l.orc_extend_and_commit.argtypes = [P, u32, sz, P, P, P, P]
         l.orc_repair.argtypes = [P, P, u32, sz, P, P, P, P, P, P]
         l.orc_repair_order.argtypes = [P, P, u32, sz, P, P, P, P, P, P, i32]
+        l.orc_extend_commit_many.argtypes = [P, u32, u32, sz, P]
+        l.orc_repair_many.argtypes = [P, P, u32, sz, P, P, u32, P]
         l.orc_init()
         _lib = l
     return _lib
@@ -189,3 +191,25 @@ def gf(field):
     n = 1 << field
     exp = np.array([l.orc_gf_exp(field, i) for i in range(min(n, 1 << 16))])
     return exp
+
+
+def extend_commit_many(ods_batch: np.ndarray) -> np.ndarray:
+    """CPU baseline: (n, k, k, share) ODSs on parallel threads -> (n, 32) DAHs."""
+    ods_batch = np.ascontiguousarray(ods_batch, dtype=np.uint8)
+    n, k, _, share = ods_batch.shape
+    out = np.zeros((n, 32), np.uint8)
+    rc = lib().orc_extend_commit_many(_p(ods_batch), n, k, share, _p(out))
+    if rc:
+        raise ValueError(f"orc_extend_commit_many rc={rc}")
+    return out
+
+
+def repair_many(eds: np.ndarray, present: np.ndarray, row_roots, col_roots, n: int) -> np.ndarray:
+    """CPU baseline: n repairs of copies of one damaged square on parallel threads."""
+    eds = np.ascontiguousarray(eds, dtype=np.uint8)
+    present = np.ascontiguousarray(present, dtype=np.uint8)
+    w, _, share = eds.shape
+    st = np.zeros(n, np.int32)
+    lib().orc_repair_many(_p(eds), _p(present), w // 2, share, _p(np.ascontiguousarray(row_roots)),
+                          _p(np.ascontiguousarray(col_roots)), n, _p(st))
+    return st

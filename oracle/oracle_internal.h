@@ -22,6 +22,8 @@ const gf_t* field_for(uint32_t n);
 void leo_encode_inplace(const gf_t* f, uint32_t m, uint8_t** w, size_t len);
 
 /* SHA-256 streaming over up to three pieces (avoids building messages). */
+void sha256_blocks(const uint8_t* blocks, size_t nblk, uint8_t out[32]);
+size_t sha256_pad(uint8_t* buf, size_t len);
 void sha256_3(const uint8_t* a, size_t la, const uint8_t* b, size_t lb, const uint8_t* c,
               size_t lc, uint8_t out[32]);
 

@@ -157,6 +157,29 @@ void sha256_3(const uint8_t* a, size_t la, const uint8_t* b, size_t lb, const ui
   }
 }
 
+/* One message already laid out with its padding in nblk whole blocks (the NMT's fixed
+ * 542-byte leaf and 181-byte node messages): one block-function call, no buffering. */
+void sha256_blocks(const uint8_t* blocks, size_t nblk, uint8_t out[32]) {
+  uint32_t st[8];
+  memcpy(st, H0, sizeof(st));
+  compress(st, blocks, nblk);
+  for (int i = 0; i < 8; i++) {
+    const uint32_t v = __builtin_bswap32(st[i]);
+    memcpy(out + 4 * i, &v, 4);
+  }
+}
+
+/* Pad a message of len bytes sitting at the start of buf (capacity >= the padded size):
+ * returns the number of 64-byte blocks. */
+size_t sha256_pad(uint8_t* buf, size_t len) {
+  const size_t nblk = (len + 8) / 64 + 1;
+  buf[len] = 0x80;
+  memset(buf + len + 1, 0, nblk * 64 - len - 1);
+  const uint64_t bits = (uint64_t)len * 8;
+  for (int i = 0; i < 8; i++) buf[nblk * 64 - 1 - i] = (uint8_t)(bits >> (8 * i));
+  return nblk;
+}
+
 void orc_sha256(const uint8_t* msg, size_t len, uint8_t out[32]) {
   sha256_3(msg, len, NULL, 0, NULL, 0, out);
 }
