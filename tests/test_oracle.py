@@ -277,3 +277,24 @@ def test_roots_order_violation(oracle):
     eds = oracle.extend(ods)
     rc, _, _ = oracle.roots(eds, check_order=True)
     assert rc == oracle.EORDER
+
+
+def test_cpu_baseline_entry_points_match_checker(oracle):
+    """bench.py's CPU baseline (independent squares / repairs per thread, SIMD block
+    functions) gives the checker's DAHs and repair outcomes bit for bit, SHA-NI and GFNI
+    paths against the scalar ones."""
+    k = 16
+    ods = np.stack([random_ods(k, s) for s in range(5)])
+    oracle.set_simd(False)
+    ref = [oracle.extend_and_commit(o, want_eds=False)[3] for o in ods]
+    oracle.set_simd(True)
+    oracle.set_threads(3)
+    got = oracle.extend_commit_many(ods)
+    assert [g.tobytes() for g in got] == ref
+    eds, rr, cr, _ = oracle.extend_and_commit(ods[0])
+    w = 2 * k
+    present = (np.random.default_rng(3).random((w, w)) < 0.6).astype(np.uint8)
+    damaged = np.where(present[..., None] == 1, eds, 0).astype(np.uint8)
+    st = oracle.repair_many(damaged, present, rr, cr, 4)
+    assert (st == oracle.repair(damaged, present, rr, cr)[0]).all()
+    oracle.set_simd(False)
