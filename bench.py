@@ -86,6 +86,9 @@ def parse():
     ap.add_argument("--k512-batch", type=int, default=32,
                     help="with --k 128: k=512 squares per step per GPU of the companion line (0 = off)")
     ap.add_argument("--k512-steps", type=int, default=5)
+    ap.add_argument("--no-riders", action="store_true",
+                    help="with --k 128: skip the config-4 (k64) and config-3 (rowshard512) riders")
+    ap.add_argument("--rider-steps", type=int, default=5)
     ap.add_argument("--mode", default="batch", choices=["batch", "sharded", "repair", "distcheck"],
                     help="batch: independent squares per GPU (configs 2, 4); sharded: one square "
                          "row-sharded over the ranks (config 3); repair: rsmt2d Repair (config 5); "
@@ -151,13 +154,33 @@ def run_distcheck(a):
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    # the riders' assembly with CPU stand-ins: the k64 split and, for the row-sharded
+    # square, the same all_to_all_single shape (k = 64 here) over gloo, timed the same way
+    riders = {}
+    if not a.no_riders:
+        riders["k64"] = _k64_fields(world, elapsed, a.steps)
+        k = 64
+        per_peer = 2 * k * k * 512 // (world * world)
+        inp = torch.full((world * per_peer,), rank, dtype=torch.uint8)
+        out = torch.empty_like(inp)
+        t_a2a = 0.0
+        if world > 1:
+            barrier()
+            t1 = time.perf_counter()
+            dist.all_to_all_single(out, inp)
+            t_a2a = time.perf_counter() - t1
+            assert all(int(out[h * per_peer]) == h for h in range(world))
+            t = torch.tensor([t_a2a], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            t_a2a = float(t.item())
+        riders["rowshard512"] = _rowshard_fields(k, world, elapsed, a.steps, t_a2a)
     if rank == 0:
         print(json.dumps({"metric": "distcheck steps/sec", "value": world * a.steps / elapsed, "unit": "steps/s",
                           "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
                           "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
                           "vs_baseline": None, "dtype": "u8", "data": "synthetic (CPU stand-in step, gloo)",
                           "config": {"workload": "launcher / rendezvous / timing contract check",
-                                     "parallelism": f"batch{world}"}}), flush=True)
+                                     "parallelism": f"batch{world}"}, **riders}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -490,6 +513,90 @@ def cpu_baseline_batch(k, distinct, dah_dev, seconds):
     }, parity
 
 
+XGMI_LINK_GBS = 153.0  # one xGMI link, per direction
+
+
+def _k64_fields(world, elapsed, steps, t_ext=None, t_com=None, B=None):
+    """Config 4 rider: 1024 independent k=64 squares in total, 1024/N per rank."""
+    f = {"workload": "config 4: 1024 independent k=64 squares in total, 1024/N per GPU (batch replay)",
+         "value": 1024 * steps / elapsed, "unit": "squares/s", "n_gpus": world, "steps": steps,
+         "ms_per_step": elapsed / steps * 1e3, "squares_per_step_per_gpu": 1024 // world, "scaling": "strong"}
+    if t_ext is not None:
+        f["rs_frac_hbm"] = 2048 * 64 * 64 * B / t_ext / 1e9 / HBM_PEAK_GBS
+        f["nmt_frac_sha_peak"] = (60 * 64 * 64 + 4 * 64 - 2) * B / t_com / SHA_MEASURED_PEAK
+    return f
+
+
+def _rowshard_fields(k, world, elapsed, steps, t_a2a):
+    """Config 3 rider: one k x k square row-sharded over the N ranks, with the all-to-all
+    alone next to SURVEY §8e's one-link estimate (bytes per peer / 153 GB/s)."""
+    per_peer = 2 * k * k * 512 // (world * world)  # (k/N rows) x (2k/N columns) x 512 B
+    return {"workload": f"config 3: one k={k} square row-sharded over {world} GPU(s), one all_to_all_single "
+                        "(column slabs) + two record all_gathers",
+            "value": steps / elapsed, "unit": "squares/s", "n_gpus": world, "steps": steps,
+            "ms_per_step": elapsed / steps * 1e3, "scaling": "strong",
+            "a2a_us": t_a2a * 1e6 if world > 1 else None,
+            "a2a_bytes_per_peer": per_peer if world > 1 else 0,
+            "a2a_gbps_per_peer": per_peer / t_a2a / 1e9 if world > 1 else None,
+            "a2a_survey_estimate_us": per_peer / (XGMI_LINK_GBS * 1e9) * 1e6 if world > 1 else None}
+
+
+def _max_over_ranks(x, dist, dev):
+    if dist is None:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def measure_rowshard(k, world, rank, local, dist, dev, steps, warmup, barrier):
+    """The run_sharded schedule as a rider of the batch line: full steps (barrier-bracketed,
+    max over ranks), then the all-to-all alone (median of 5, max over ranks)."""
+    from celestia_eds import default_context
+    from celestia_eds.sharded import DeviceSteps, LocalComm, ShardedSquare, TorchComm
+    from celestia_eds.testfactory import random_ods
+    ctx = default_context(local)
+    dsteps = DeviceSteps(ctx, local)
+    sq = ShardedSquare(k, rank, world, dsteps)
+    lo, hi = sq.row_range()
+    sq.ods_rows.copy_(torch.from_numpy(np.ascontiguousarray(random_ods(k, 512)[lo:hi])))
+    comm = TorchComm() if dist is not None else None
+
+    def step():
+        if comm is not None:
+            sq.run(comm)
+        else:
+            LocalComm.run([sq])
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = _max_over_ranks(time.perf_counter() - t0, dist, dev)
+    sq.check_status()
+    t_a2a = 0.0
+    if comm is not None:
+        ts = []
+        for _ in range(5):
+            torch.cuda.synchronize()
+            barrier()
+            t1 = time.perf_counter()
+            with sq.scope():
+                sq.exchange(comm)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t1)
+        t_a2a = _max_over_ranks(sorted(ts)[2], dist, dev)
+    del sq
+    return _rowshard_fields(k, world, elapsed, steps, t_a2a)
+
+
 def _measure_batch(ctx, local, rank, k, B, steps, warmup, n_distinct, layout, phase_reps, barrier, dist, dev):
     """Time `steps` batch steps of B k x k squares resident in HBM (barrier + synchronize
     on both sides, max over ranks), then the RS and NMT phases alone with HIP events on
@@ -713,6 +820,18 @@ def main():
         sb = None
     else:
         dah128 = None
+    if a.k == 128 and not a.no_riders:
+        # Configs 4 and 3 in the same run, so one driver N-GPU command measures configs 2, 3
+        # and 4: 1024 k=64 squares split over the ranks, and one k=512 square row-sharded
+        # over all ranks through RCCL (all_to_all_single) with its exchange timed alone.
+        torch.cuda.empty_cache()
+        m4 = _measure_batch(ctx, local, rank, 64, 1024 // world, a.rider_steps, 2, 4, a.input, 3, barrier, dist,
+                            dev)
+        result["k64"] = _k64_fields(world, m4["elapsed"], a.rider_steps, m4["t_ext"], m4["t_com"], 1024 // world)
+        del m4
+        torch.cuda.empty_cache()
+        result["rowshard512"] = measure_rowshard(512, world, rank, local, dist, dev, a.rider_steps, 2, barrier)
+        torch.cuda.empty_cache()
     if rank == 0 and world == 1 and a.k == 128 and not a.no_host_io:
         result["host_io"] = measure_host_io(ctx, a.k)
     if rank == 0 and world == 1 and not a.no_cpu:

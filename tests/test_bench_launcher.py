@@ -34,3 +34,18 @@ def test_launcher_two_ranks():
 def test_single_rank_no_relaunch():
     out = _run(["--mode", "distcheck", "--steps", "2", "--warmup", "0"])
     assert len(out) == 1 and out[0]["n_gpus"] == 1
+
+
+def test_riders_in_multi_rank_line():
+    """One N-rank command carries configs 4 and 3 as riders (k64: 1024/N squares per rank;
+    rowshard512: the row-sharded square's all_to_all_single, timed alone, beside SURVEY
+    §8e's one-link estimate), with n_gpus = N. Here over gloo with CPU stand-in steps."""
+    out = _run(["--gpus", "4", "--mode", "distcheck", "--steps", "2", "--warmup", "1"])
+    assert len(out) == 1, out
+    r = out[0]
+    assert r["n_gpus"] == 4
+    assert r["k64"]["n_gpus"] == 4 and r["k64"]["squares_per_step_per_gpu"] == 256
+    rs = r["rowshard512"]
+    assert rs["n_gpus"] == 4 and rs["scaling"] == "strong"
+    assert rs["a2a_bytes_per_peer"] == 2 * 64 * 64 * 512 // 16
+    assert rs["a2a_us"] > 0 and rs["a2a_survey_estimate_us"] > 0
