@@ -167,7 +167,13 @@ cel_status cel_device_name(cel_ctx* ctx, char* buf, size_t len) {
   if (!ctx || !buf || !len) return CEL_EINVAL;
   hipDeviceProp_t p;
   if (hipGetDeviceProperties(&p, ctx->device) != hipSuccess) return CEL_EDEVICE;
-  std::snprintf(buf, len, "%s (%s)", p.name, p.gcnArchName);
+  // the marketing name can be empty on a box (a driver without the product table): then
+  // the PCI device id stands in for it
+  if (p.name[0])
+    std::snprintf(buf, len, "%s (%s, %d CUs)", p.name, p.gcnArchName, p.multiProcessorCount);
+  else
+    std::snprintf(buf, len, "AMD GPU %04x:%02x:%02x (%s, %d CUs)", p.pciDomainID, p.pciBusID, p.pciDeviceID,
+                  p.gcnArchName, p.multiProcessorCount);
   return CEL_OK;
 }
 
