@@ -89,6 +89,10 @@ def parse():
     ap.add_argument("--no-riders", action="store_true",
                     help="with --k 128: skip the config-4 (k64) and config-3 (rowshard512) riders")
     ap.add_argument("--rider-steps", type=int, default=5)
+    ap.add_argument("--rehearse", action="store_true",
+                    help="multi-rank rehearsal on a one-GPU box: every rank on cuda:0, gloo instead of RCCL "
+                         "(collectives staged through host memory); exercises the N-rank code path, its "
+                         "numbers are not multi-GPU measurements")
     ap.add_argument("--mode", default="batch", choices=["batch", "sharded", "repair", "distcheck"],
                     help="batch: independent squares per GPU (configs 2, 4); sharded: one square "
                          "row-sharded over the ranks (config 3); repair: rsmt2d Repair (config 5); "
@@ -202,15 +206,15 @@ def run_sharded(a):
     hashes its slab, two all-gathers of 96-byte records and a combine give the roots
     and the DAH on every rank. At N = 1 the same schedule runs without collectives."""
     world, rank, local = _dist_env()
+    local = _rank_device(local)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     from celestia_eds import default_context
-    from celestia_eds.sharded import DeviceSteps, LocalComm, ShardedSquare, TorchComm
+    from celestia_eds.sharded import DeviceSteps, LocalComm, ShardedSquare
     from celestia_eds.testfactory import random_ods
     dist = None
     if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        dist = _init_dist(dev)
     k = a.k
     ctx = default_context(local)
     steps = DeviceSteps(ctx, local)
@@ -218,7 +222,7 @@ def run_sharded(a):
     ods = random_ods(k, 512)
     lo, hi = sq.row_range()
     sq.ods_rows.copy_(torch.from_numpy(np.ascontiguousarray(ods[lo:hi])))
-    comm = TorchComm() if dist is not None else None
+    comm = _comm() if dist is not None else None
 
     def step():
         if comm is not None:
@@ -241,11 +245,7 @@ def run_sharded(a):
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = _max_over_ranks(time.perf_counter() - t0, dist, dev)
     sq.check_status()
     # rank-local phase timing (HIP events on the launch stream of the device steps)
     cur = steps.stream
@@ -541,10 +541,31 @@ def _rowshard_fields(k, world, elapsed, steps, t_a2a):
             "a2a_survey_estimate_us": per_peer / (XGMI_LINK_GBS * 1e9) * 1e6 if world > 1 else None}
 
 
+REHEARSE = False  # set by main() from --rehearse
+
+
+def _rank_device(local):
+    return 0 if REHEARSE else local
+
+
+def _init_dist(dev):
+    import torch.distributed as dist
+    if REHEARSE:
+        dist.init_process_group("gloo")
+    else:
+        dist.init_process_group("nccl", device_id=dev)
+    return dist
+
+
+def _comm():
+    from celestia_eds.sharded import StagedComm, TorchComm
+    return StagedComm() if REHEARSE else TorchComm()
+
+
 def _max_over_ranks(x, dist, dev):
     if dist is None:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    t = torch.tensor([x], dtype=torch.float64, device="cpu" if REHEARSE else dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -553,14 +574,14 @@ def measure_rowshard(k, world, rank, local, dist, dev, steps, warmup, barrier):
     """The run_sharded schedule as a rider of the batch line: full steps (barrier-bracketed,
     max over ranks), then the all-to-all alone (median of 5, max over ranks)."""
     from celestia_eds import default_context
-    from celestia_eds.sharded import DeviceSteps, LocalComm, ShardedSquare, TorchComm
+    from celestia_eds.sharded import DeviceSteps, LocalComm, ShardedSquare
     from celestia_eds.testfactory import random_ods
     ctx = default_context(local)
     dsteps = DeviceSteps(ctx, local)
     sq = ShardedSquare(k, rank, world, dsteps)
     lo, hi = sq.row_range()
     sq.ods_rows.copy_(torch.from_numpy(np.ascontiguousarray(random_ods(k, 512)[lo:hi])))
-    comm = TorchComm() if dist is not None else None
+    comm = _comm() if dist is not None else None
 
     def step():
         if comm is not None:
@@ -621,11 +642,7 @@ def _measure_batch(ctx, local, rank, k, B, steps, warmup, n_distinct, layout, ph
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = _max_over_ranks(time.perf_counter() - t0, dist, dev)
     status = sb.status.cpu().numpy()
     assert (status == 0).all(), f"device reported status {status}"
 
@@ -706,7 +723,9 @@ def measure_host_io(ctx, k, n=16, reps=3):
 
 
 def main():
+    global REHEARSE
     a = parse()
+    REHEARSE = a.rehearse
     world, rank, local = _dist_env()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch(a))
@@ -716,12 +735,12 @@ def main():
         return run_sharded(a)
     if a.mode == "repair":
         return run_repair(a)
+    local = _rank_device(local)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        dist = _init_dist(dev)
 
     from celestia_eds import default_context
 
@@ -838,6 +857,8 @@ def main():
         dah_dev = dah128 if dah128 is not None else sb.dah.cpu().numpy()
         result["cpu_baseline"], parity = cpu_baseline_batch(k, distinct, dah_dev, a.cpu_seconds)
         result["parity_vs_cpu"] = bool(parity)
+    if REHEARSE:
+        result["config"]["rehearsal"] = "all ranks on cuda:0, gloo with host staging: not a multi-GPU measurement"
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist is not None:

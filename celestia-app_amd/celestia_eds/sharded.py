@@ -49,6 +49,32 @@ class TorchComm:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
 
 
+class StagedComm:
+    """The same collectives over gloo on host copies of device tensors (gloo has no
+    all_to_all for device tensors): the multi-rank rehearsal of the RCCL path with every
+    rank on one GPU (bench.py --rehearse, the two-rank GPU test)."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+
+    def all_to_all(self, out, inp):
+        h_out = out.cpu()
+        self.dist.all_to_all_single(h_out, inp.cpu(), group=self.group)
+        out.copy_(h_out)
+
+    def all_gather(self, out, inp):
+        h_out = out.cpu()
+        self.dist.all_gather_into_tensor(h_out, inp.cpu(), group=self.group)
+        out.copy_(h_out)
+
+    def all_reduce_max(self, t):
+        h = t.cpu()
+        self.dist.all_reduce(h, op=self.dist.ReduceOp.MAX, group=self.group)
+        t.copy_(h)
+
+
 class DeviceSteps:
     """Per-rank device steps through the C ABI (device tensors, current HIP stream)."""
 

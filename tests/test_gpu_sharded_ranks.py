@@ -13,35 +13,12 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-class StagedComm:
-    """torch.distributed gloo collectives on host copies of device tensors."""
-
-    def __init__(self):
-        import torch.distributed as dist
-        self.dist = dist
-
-    def all_to_all(self, out, inp):
-        h_out = out.cpu()
-        self.dist.all_to_all_single(h_out, inp.cpu())
-        out.copy_(h_out)
-
-    def all_gather(self, out, inp):
-        h_out = out.cpu()
-        self.dist.all_gather_into_tensor(h_out, inp.cpu())
-        out.copy_(h_out)
-
-    def all_reduce_max(self, t):
-        h = t.cpu()
-        self.dist.all_reduce(h, op=self.dist.ReduceOp.MAX)
-        t.copy_(h)
-
-
 def _worker(rank, world, port, k, outdir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     import torch
     import torch.distributed as dist
     from celestia_eds import default_context
-    from celestia_eds.sharded import DeviceSteps, ShardedSquare
+    from celestia_eds.sharded import DeviceSteps, ShardedSquare, StagedComm
     from celestia_eds.testfactory import random_ods
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
