@@ -413,6 +413,7 @@ def run_repair(a):
         t_cpu += time.perf_counter() - t1
         n_cpu += len(st)
         assert (st == 0).all()
+    byz = measure_byzantine_repair(ctx, eds, rr, cr, present, k) if a.repair_input == "device" else None
     value = a.steps / elapsed
     print(json.dumps({
         "metric": "rsmt2d Repair squares/sec (k=%d, p=%.2f)" % (k, a.repair_p),
@@ -435,7 +436,45 @@ def run_repair(a):
                          "sample": f"{n_cpu} repairs of the same damaged square, one per thread (C restatement: "
                                    "crossword sweeps, Leopard FWHT decoder, re-encode and root checks)",
                          "one_thread_ms_per_repair": t_one * 1e3},
+        "byzantine": byz,
     }), flush=True)
+
+
+def measure_byzantine_repair(ctx, eds, rr, cr, present, k, reps=3):
+    """Config 5 (v): the same mask with one corrupted known cell whose row and column are
+    both incomplete, so a decode meets it: the pass-parallel schedule finds a failing check
+    and the square is replayed in rsmt2d's sweep order. Time per repair
+    (EDS resident, damaged copy restored outside the clock) and the reported axis."""
+    import ctypes
+    w = 2 * k
+    pres = present.copy()
+    r, c = 40, 77
+    pres[r, c] = 1
+    pres[r, 3] = pres[200, c] = 0
+    bad = eds.copy()
+    bad[r, c, 300] ^= 0x21
+    bad[pres == 0] = 0
+    d_bad = torch.from_numpy(bad).cuda()
+    d_work = torch.empty_like(d_bad)
+    rra, cra = np.ascontiguousarray(rr), np.ascontiguousarray(cr)
+    P = lambda x: x.ctypes.data_as(ctypes.c_void_p)
+    ts, axis = [], None
+    for i in range(reps + 1):
+        d_work.copy_(d_bad)
+        torch.cuda.synchronize()
+        m = pres.copy()
+        ba, bi = ctypes.c_int32(-1), ctypes.c_int32(-1)
+        t0 = time.perf_counter()
+        st = ctx.lib.cel_dev_repair(ctx.handle, ctypes.c_void_p(d_work.data_ptr()), P(m), k, P(rra), P(cra),
+                                    ctypes.byref(ba), ctypes.byref(bi), None, None)
+        if i:
+            ts.append(time.perf_counter() - t0)
+        axis = (ba.value, bi.value)
+        assert st == 7, st  # CEL_EBYZANTINE
+    del d_bad, d_work
+    return {"workload": f"the same k={k} mask with one corrupted known cell (rsmt2d sweep-order replay)",
+            "ms_per_repair": sorted(ts)[len(ts) // 2] * 1e3, "status": "ErrByzantineData",
+            "axis": axis[0], "index": axis[1]}
 
 
 def _oracle():
