@@ -1298,11 +1298,14 @@ static cel_status repair_exact(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>
     if (!progress) break;
   }
   // device: the starting mask again, every level's axis lists in one upload (each axis is
-  // solved once: at most 2W entries), then the levels in order on the main stream
+  // solved once: at most 2W entries), then the levels in order on the main stream. The
+  // register decoder takes a level's rows and columns in one launch (direction in bit 30
+  // of each entry); the LDS path gathers one direction per launch.
+  const bool in_square = rs_decode_axis_supported(W, kShare);
   std::vector<int32_t> lists;
   struct Group {
     uint32_t off, n;
-    int is_col;
+    int is_col;  // -1: mixed
   };
   std::vector<Group> groups;
   {
@@ -1310,12 +1313,20 @@ static cel_status repair_exact(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>
     by[0].resize(nlevels + 1);
     by[1].resize(nlevels + 1);
     for (size_t t = 0; t < solves.size(); t++) by[solves[t].is_col][level[t]].push_back(solves[t].idx);
-    for (int32_t L = 1; L <= nlevels; L++)
+    for (int32_t L = 1; L <= nlevels; L++) {
+      if (in_square) {
+        const uint32_t off = (uint32_t)lists.size();
+        for (int d = 0; d < 2; d++)
+          for (int32_t i : by[d][L]) lists.push_back(d ? (int32_t)((uint32_t)i | (1u << 30)) : i);
+        if ((uint32_t)lists.size() > off) groups.push_back({off, (uint32_t)lists.size() - off, -1});
+        continue;
+      }
       for (int d = 0; d < 2; d++)
         if (!by[d][L].empty()) {
           groups.push_back({(uint32_t)lists.size(), (uint32_t)by[d][L].size(), d});
           lists.insert(lists.end(), by[d][L].begin(), by[d][L].end());
         }
+    }
   }
   hipError_t e;
   cel_status st;
@@ -1327,7 +1338,6 @@ static cel_status repair_exact(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>
       (!lists.empty() && (e = hipMemcpyAsync(b.idx, b.hidx, lists.size() * 4, hipMemcpyHostToDevice, b.main)) != hipSuccess) ||
       (e = hipMemsetAsync(b.flags, 0, 2 * (size_t)W * 4, b.main)) != hipSuccess)
     return hip_fail(ctx, e, "H2D");
-  const bool in_square = rs_decode_axis_supported(W, kShare);
   for (const Group& g : groups) {
     const int32_t* idx = b.idx + g.off;
     if ((st = fuzz(ctx, b.main)) != CEL_OK) return st;

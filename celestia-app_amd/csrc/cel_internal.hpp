@@ -154,9 +154,10 @@ size_t decode_workspace_size(uint32_t naxes, uint32_t n);
 bool rs_decode_axis_supported(uint32_t n, uint32_t len);
 hipError_t launch_rs_decode_axis(uint8_t* shards, const uint8_t* present, uint32_t naxes, uint32_t n, uint32_t len,
                                  const uint32_t* mul8, hipStream_t s);
-// The repair's solve of naxes axes (rows if !is_col, else columns, indices idx) of a
-// W x W square of 512-byte cells in place: erased cells decoded straight into the square,
-// the axes marked present in mask (W = 32 .. 256, the register decoder's range).
+// The repair's solve of naxes axes (rows if is_col == 0, columns if 1, indices idx; with
+// is_col < 0 every entry carries its direction in bit 30) of a W x W square of 512-byte
+// cells in place: erased cells decoded straight into the square, the axes marked present
+// in mask (W = 32 .. 256, the register decoder's range).
 hipError_t launch_rs_decode_in_square(uint8_t* eds, uint8_t* mask, uint32_t W, const int32_t* idx, int is_col,
                                       uint32_t naxes, const uint32_t* mul8, hipStream_t s);
 

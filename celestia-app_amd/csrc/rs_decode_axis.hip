@@ -120,7 +120,10 @@ __global__ __launch_bounds__(256, 2) void k_rs_decode_axis(uint8_t* __restrict__
   uint8_t* pa;
   uint32_t sst, pst;  // shard stride (bytes), presence stride
   if (idx) {
-    const uint32_t ax = (uint32_t)idx[blockIdx.x];
+    // is_col < 0: each entry names its own direction (bit 30 set = column)
+    const uint32_t e = (uint32_t)idx[blockIdx.x];
+    const uint32_t ax = e & 0x3FFFFFFFu;
+    if (is_col < 0) is_col = (int)((e >> 30) & 1u);
     axis = shards + (is_col ? (uint64_t)ax * len : (uint64_t)ax * W * len);
     sst = is_col ? W * len : len;
     pa = present + (is_col ? (uint64_t)ax : (uint64_t)ax * W);
