@@ -50,6 +50,16 @@ constexpr uint32_t merged_lm(uint32_t s1, uint32_t s2) {
 // multiply (~10 VALU per dword). Layers D = 1, 2, 4 (twiddles differ inside a block) keep
 // the v_perm multiply. For K = 128: 6 v_perm layers, 7 bit-sliced layers, 32 transposes.
 
+// Scheduling fence in the v_perm layers every CEL_AX_SB butterflies (A/B knob; 1 = after
+// every butterfly, 0 = none: the compiler may interleave a whole layer).
+#ifndef CEL_AX_SB
+#define CEL_AX_SB 1
+#endif
+template <int J>
+__device__ __forceinline__ void vperm_fence() {
+  if constexpr (CEL_AX_SB > 0 && (J + 1) % (CEL_AX_SB > 0 ? CEL_AX_SB : 1) == 0) __builtin_amdgcn_sched_barrier(0);
+}
+
 template <int K>
 __device__ __forceinline__ void transform_hyb(uint32_t (&w)[K]) {
   constexpr int LOGK = __builtin_ctz(K);
@@ -67,7 +77,7 @@ __device__ __forceinline__ void transform_hyb(uint32_t (&w)[K]) {
         w[a + D] ^= w[a];
         m.muladd(w[a], w[a + D], m7, m3);
         pin(w[a], w[a + D]);
-        __builtin_amdgcn_sched_barrier(0);
+        vperm_fence<base / 2 + decltype(j)::value>();
       });
     });
   });
@@ -127,7 +137,7 @@ __device__ __forceinline__ void transform_hyb(uint32_t (&w)[K]) {
         m.muladd(w[a], w[a + D], m7, m3);
         w[a + D] ^= w[a];
         pin(w[a], w[a + D]);
-        __builtin_amdgcn_sched_barrier(0);
+        vperm_fence<base / 2 + decltype(j)::value>();
       });
     });
   });
