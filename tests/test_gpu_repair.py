@@ -22,7 +22,7 @@ def repair(ctx, eds, present, rr, cr):
     return sq.cells
 
 
-@pytest.mark.parametrize("k", [4, 32, 128])
+@pytest.mark.parametrize("k", [1, 2, 4, 32, 128])
 @pytest.mark.parametrize("quadrant", [0, 1, 2, 3])
 def test_single_quadrant(ctx, oracle, k, quadrant):
     eds, rr, cr = setup(oracle, k)
@@ -462,12 +462,14 @@ def _byz_case(oracle, k, seed):
     return bad, present, rr, cr
 
 
-@pytest.mark.parametrize("k,seed", [(8, 0), (32, 0), (32, 2), (128, 0)])
+@pytest.mark.parametrize("k,seed", [(8, 0), (32, 0), (32, 2), (128, 0), (256, 2)])
 def test_sweep_order_byzantine(ctx, oracle, k, seed):
     """Cases where rsmt2d's sweep (row i, then column i) reports a different byzantine axis
     than all-rows-then-all-columns passes would: the device (pass-parallel schedule, then
     the exact replay in rsmt2d's order) reports the oracle's sweep-order outcome, Shares
-    and mask included. k = 8: gather -> LDS decoder; k >= 16: the in-square decoder."""
+    and mask included. k = 8: gather -> LDS decoder; k = 32, 128: the in-square register
+    decoder (a level's rows and columns in one launch); k = 256: GF(2^16), gather -> LDS
+    decoder -> scatter per direction."""
     from celestia_eds import _lib
     bad, present, rr, cr = _byz_case(oracle, k, seed)
     damaged = np.where(present[..., None] == 1, bad, 0).astype(np.uint8)
@@ -501,8 +503,7 @@ def test_repair_schedule_fuzz(ctx, oracle, k):
                     assert st == _lib.OK and np.array_equal(cells, eds), fseed
                 else:
                     assert st == _lib.EUNREPAIRABLE, (fseed, st)
-            if k <= 128:
-                bad, present, brr, bcr = _byz_case(oracle, k, 0)
-                _assert_same_outcome(ctx, oracle, bad, present, brr, bcr)
+            bad, present, brr, bcr = _byz_case(oracle, k, 0 if k <= 128 else 2)
+            _assert_same_outcome(ctx, oracle, bad, present, brr, bcr)
     finally:
         ctx.lib.cel_debug_schedule_fuzz(ctx.handle, 0, 0)
