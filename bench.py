@@ -753,6 +753,17 @@ def measure_host_io(ctx, k, n=16, reps=3):
         for _ in range(10):
             one()
         out["single_square_parity_only_ms"] = (time.perf_counter() - t0) / 10 * 1e3
+
+        # the header alone (da.ComputeDataAvailabilityHeader): what PrepareProposal /
+        # ProcessProposal keep; no EDS copied back
+        def dah_only():
+            ctx.check(ctx.lib.cel_extend_batch(ctx.handle, P(ods), 1, k, 512, None, P(rr), P(cr), P(dah), P(st),
+                                               _lib.FLAG_ORDER_CHECK))
+        dah_only()
+        t0 = time.perf_counter()
+        for _ in range(10):
+            dah_only()
+        out["single_square_dah_only_ms"] = (time.perf_counter() - t0) / 10 * 1e3
     finally:
         ctx.lib.cel_host_free(p_ods)
         ctx.lib.cel_host_free(p_eds)

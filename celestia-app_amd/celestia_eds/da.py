@@ -2,6 +2,8 @@
 
   ExtendShares(shares)            :65-75   -> one device pass (RS + NMT roots)
   NewDataAvailabilityHeader(eds)  :44-63
+  ComputeDataAvailabilityHeader   both at once with no EDS copy-back (the DAH is all that
+                                  app/prepare_proposal.go / process_proposal.go keep)
   DataAvailabilityHeader          :33-41, Hash :92-108, ValidateBasic :134-162,
                                   IsZero :164-170, SquareSize :205-207, Equals :86-88
   MinDataAvailabilityHeader       :179-190, MinShares :193-196
@@ -67,6 +69,31 @@ def _extend(shares, ctx=None, order_check=True):
 def ExtendShares(shares):
     """da.ExtendShares: [][]byte (k*k shares) -> *rsmt2d.ExtendedDataSquare."""
     return _extend(shares)
+
+
+def ComputeDataAvailabilityHeader(shares, ctx=None):
+    """NewDataAvailabilityHeader(ExtendShares(shares)) for callers that keep only the DAH:
+    app/prepare_proposal.go:61-92 and app/process_proposal.go:138-156 extend the square,
+    build the DAH and use nothing but dah.Hash() ("the eds is not returned here"). One
+    device pass with no EDS copied back (cel_extend_shares with eds_out = NULL): the ODS
+    goes up, the 4k roots and the hash come down. Same errors as ExtendShares."""
+    ctx = ctx or _lib.default_context()
+    n = len(shares)
+    if not _is_pow2(n):
+        raise CelError(_lib.ENOTPOW2, f"number of shares is not a power of 2: got {n}")
+    if isinstance(shares, np.ndarray):
+        ods = np.ascontiguousarray(shares, np.uint8).reshape(-1)
+    else:
+        ods = np.frombuffer(b"".join(bytes(s) for s in shares), np.uint8).copy()
+    k = SquareSize(n)
+    rr = np.zeros((2 * k, _lib.NMT_NODE_SIZE), np.uint8)
+    cr = np.zeros((2 * k, _lib.NMT_NODE_SIZE), np.uint8)
+    dah = np.zeros(32, np.uint8)
+    ctx.check(ctx.lib.cel_extend_shares(ctx.handle, _p(ods), n, SHARE_SIZE, None, _p(rr), _p(cr), _p(dah),
+                                        _lib.FLAG_ORDER_CHECK))
+    out = DataAvailabilityHeader([r.tobytes() for r in rr], [c.tobytes() for c in cr])
+    out.hash = dah.tobytes()
+    return out
 
 
 class DataAvailabilityHeader:

@@ -48,6 +48,28 @@ def test_dah_known_answers(ctx, golden):
         assert eds._dah.hex() == kat[key]
 
 
+def test_compute_dah_without_eds(ctx, golden, block408_ods):
+    """ComputeDataAvailabilityHeader (no EDS copied back, the PrepareProposal /
+    ProcessProposal shape) equals NewDataAvailabilityHeader(ExtendShares(...)): the DAH known
+    answers, block 408's data root, and the same error as ExtendShares."""
+    import pytest as _pytest
+    from celestia_eds import CelError, _lib, da
+    kat = golden["dah_known_answers"]
+    for k, key in ((2, "typical_k2"), (128, "max_k128")):
+        dah = da.ComputeDataAvailabilityHeader(list(constant_ods(k).reshape(-1, 512)))
+        assert dah.Hash().hex() == kat[key] and len(dah.RowRoots) == 2 * k
+        dah.hash = b""  # recomputed from the returned roots
+        assert dah.Hash().hex() == kat[key]
+    ods = random_ods(32, 9)
+    ref = da.NewDataAvailabilityHeader(da.ExtendShares(list(ods.reshape(-1, 512))))
+    got = da.ComputeDataAvailabilityHeader(list(ods.reshape(-1, 512)))
+    assert got.RowRoots == ref.RowRoots and got.ColumnRoots == ref.ColumnRoots and got.Hash() == ref.Hash()
+    assert da.ComputeDataAvailabilityHeader(block408_ods.reshape(-1, 512)).Hash().hex() == golden["block408"]["data_hash"]
+    with _pytest.raises(CelError) as ei:
+        da.ComputeDataAvailabilityHeader([bytes(512)] * 5)
+    assert ei.value.status == _lib.ENOTPOW2 and "got 5" in str(ei.value)
+
+
 def test_min_dah_validate_and_square_size(ctx):
     from celestia_eds import da
     dah = da.MinDataAvailabilityHeader()
