@@ -140,7 +140,8 @@ void orc_merkle_root(const uint8_t* items, uint32_t n, size_t item_len, uint8_t 
 }
 
 void orc_dah_hash(const uint8_t* row_roots, const uint8_t* col_roots, uint32_t w, uint8_t out[32]) {
-  uint8_t* all = (uint8_t*)malloc((size_t)((2 * w) ? (2 * w) : 1) * ORC_NODE);
+  const size_t nroots = w ? (size_t)2 * w : 1;
+  uint8_t* all = (uint8_t*)malloc(nroots * ORC_NODE);
   memcpy(all, row_roots, (size_t)w * ORC_NODE);
   memcpy(all + (size_t)w * ORC_NODE, col_roots, (size_t)w * ORC_NODE);
   merkle_rec(all, 2 * w, ORC_NODE, out);
@@ -151,9 +152,11 @@ void orc_dah_hash(const uint8_t* row_roots, const uint8_t* col_roots, uint32_t w
 
 static int encode_axis(uint32_t k, size_t share, const uint8_t* src, size_t sstride, uint8_t* dst,
                        size_t dstride) {
+  if (k == 0 || share == 0) return ORC_EINVAL;
   uint8_t* d = (uint8_t*)malloc((size_t)k * share);
+  memcpy(d, src, share);
   uint8_t* p = (uint8_t*)malloc((size_t)k * share);
-  for (uint32_t i = 0; i < k; i++) memcpy(d + (size_t)i * share, src + (size_t)i * sstride, share);
+  for (uint32_t i = 1; i < k; i++) memcpy(d + (size_t)i * share, src + (size_t)i * sstride, share);
   int rc = orc_rs_encode(k, share, d, p);
   if (rc == ORC_OK)
     for (uint32_t i = 0; i < k; i++) memcpy(dst + (size_t)i * dstride, p + (size_t)i * share, share);
