@@ -27,7 +27,7 @@ EXPORTS = [
     "cel_extend_shares", "cel_extend_batch", "cel_dev_workspace_size", "cel_dev_extend_batch",
     "cel_dev_extend_only", "cel_dev_commit_only", "cel_dev_place_ods", "cel_dev_decode", "cel_host_alloc", "cel_host_free", "cel_codec_encode", "cel_codec_decode",
     "cel_codec_max_chunks", "cel_codec_name", "cel_codec_validate_chunk_size", "cel_axis_root",
-    "cel_nmt_root", "cel_dah_hash", "cel_merkle_hash_slices", "cel_repair", "cel_dev_repair", "cel_debug_schedule_fuzz", "cel_dev_shard_workspace_size", "cel_dev_shard_rows",
+    "cel_nmt_root", "cel_dah_hash", "cel_merkle_hash_slices", "cel_repair", "cel_dev_repair", "cel_debug_schedule_fuzz", "cel_debug_repair_plan", "cel_dev_shard_workspace_size", "cel_dev_shard_rows",
     "cel_dev_shard_cols", "cel_dev_shard_finish", "cel_square_construct", "cel_square_last_error", "cel_square_tx_range",
     "cel_axis_trees", "cel_dah_tree", "cel_nmt_prove_range", "cel_merkle_aunts", "cel_commitment_paths",
     "cel_get_commitment", "cel_subtree_root_coordinates",
@@ -82,6 +82,7 @@ def load():
             "cel_repair": (i32, [P, P, P, u32, u32, P, P, P, P, P, P]),
             "cel_dev_repair": (i32, [P, P, P, u32, P, P, P, P, P, P]),
             "cel_debug_schedule_fuzz": (i32, [P, u64, u32]),
+            "cel_debug_repair_plan": (i32, [P, u32, P, P, P, P, P]),
             "cel_dev_shard_workspace_size": (sz, [u32, u32]),
             "cel_dev_shard_rows": (i32, [P, P, u32, u32, P, P]),
             "cel_dev_shard_cols": (i32, [P, P, u32, u32, u32, P, P, P, P, P, u32]),

@@ -1244,13 +1244,26 @@ static cel_status verify_square(cel_ctx* ctx, RepairBufs& b, uint32_t k, int pen
 // launch; level by level the device sees every axis exactly as rsmt2d's sequence does.
 // hm0: the mask the repair started from; cells present in it still hold their bytes
 // (every decoder stores erased cells only).
-static cel_status repair_exact(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>& hm, uint32_t k, const Verify& base,
-                               const RepairOut& out) {
-  const Range range("repair.exact");
+// rsmt2d's sweeps over the mask alone (every solve completes its axis): the solve
+// sequence, each solve's level and the check order (SOLVE, then the ORTH axes it
+// completes, ascending); cnt = known cells per axis at the end.
+struct SweepPlan {
+  std::vector<Solve> solves;
+  std::vector<int32_t> level;
+  std::vector<Check> order;
+  std::vector<uint32_t> cnt[2];
+  int32_t nlevels = 0;
+  bool solved = false;
+};
+
+static SweepPlan plan_sweeps(const std::vector<uint8_t>& hm, uint32_t k) {
   const uint32_t W = 2 * k;
   const size_t cells = (size_t)W * W;
+  SweepPlan p;
   std::vector<uint8_t> m(hm);
-  std::vector<uint32_t> cnt[2] = {std::vector<uint32_t>(W, 0), std::vector<uint32_t>(W, 0)};
+  p.cnt[0].assign(W, 0);
+  p.cnt[1].assign(W, 0);
+  auto& cnt = p.cnt;
   size_t total = 0;
   for (uint32_t i = 0; i < W; i++)
     for (uint32_t j = 0; j < W; j++)
@@ -1260,12 +1273,8 @@ static cel_status repair_exact(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>
         total++;
       }
   std::vector<int32_t> lvl_of(cells, 0);
-  std::vector<Solve> solves;
-  std::vector<int32_t> level;
-  std::vector<Check> order;
-  int32_t nlevels = 0;
-  bool solved = total == cells;
-  while (!solved) {
+  p.solved = total == cells;
+  while (!p.solved) {
     bool progress = false;
     for (uint32_t i = 0; i < W; i++)
       for (int d = 0; d < 2; d++) {
@@ -1277,26 +1286,41 @@ static cel_status repair_exact(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>
           if (m[c] && lvl_of[c] > L) L = lvl_of[c];
         }
         L++;
-        const int32_t si = (int32_t)solves.size();
-        order.push_back({Check::SOLVE, d, (int32_t)i, si});
+        const int32_t si = (int32_t)p.solves.size();
+        p.order.push_back({Check::SOLVE, d, (int32_t)i, si});
         for (uint32_t j = 0; j < W; j++) {
           const size_t c = base_c + j * step;
           if (m[c]) continue;
-          if (cnt[!d][j] == W - 1) order.push_back({Check::ORTH, !d, (int32_t)j, si});
+          if (cnt[!d][j] == W - 1) p.order.push_back({Check::ORTH, !d, (int32_t)j, si});
           m[c] = 1;
           lvl_of[c] = L;
           cnt[!d][j]++;
           total++;
         }
         cnt[d][i] = W;
-        solves.push_back({d, (int32_t)i});
-        level.push_back(L);
-        if (L > nlevels) nlevels = L;
+        p.solves.push_back({d, (int32_t)i});
+        p.level.push_back(L);
+        if (L > p.nlevels) p.nlevels = L;
         progress = true;
       }
-    if (total == cells) solved = true;
+    if (total == cells) p.solved = true;
     if (!progress) break;
   }
+  return p;
+}
+
+static cel_status repair_exact(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>& hm, uint32_t k, const Verify& base,
+                               const RepairOut& out) {
+  const Range range("repair.exact");
+  const uint32_t W = 2 * k;
+  const size_t cells = (size_t)W * W;
+  const SweepPlan plan = plan_sweeps(hm, k);
+  const std::vector<Solve>& solves = plan.solves;
+  const std::vector<int32_t>& level = plan.level;
+  const std::vector<Check>& order = plan.order;
+  const int32_t nlevels = plan.nlevels;
+  const bool solved = plan.solved;
+  const auto& cnt = plan.cnt;
   // device: the starting mask again, every level's axis lists in one upload (each axis is
   // solved once: at most 2W entries), then the levels in order on the main stream. The
   // register decoder takes a level's rows and columns in one launch (direction in bit 30
@@ -1589,6 +1613,25 @@ cel_status cel_repair(cel_ctx* ctx, uint8_t* eds, uint8_t* present, uint32_t k, 
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "sync");
   std::memcpy(present, hm.data(), cells);
   return st;
+}
+
+cel_status cel_debug_repair_plan(const uint8_t* present, uint32_t k, int32_t* solve_axis, int32_t* solve_index,
+                                 int32_t* solve_level, uint32_t* nsolves, int32_t* solved) {
+  if (!present || !solve_axis || !solve_index || !solve_level || !nsolves || !solved || !k || (k & (k - 1)) ||
+      k > 512)
+    return CEL_EINVAL;
+  const size_t cells = (size_t)4 * k * k;
+  std::vector<uint8_t> hm(cells);
+  for (size_t i = 0; i < cells; i++) hm[i] = present[i] != 0;
+  const SweepPlan p = plan_sweeps(hm, k);
+  for (size_t t = 0; t < p.solves.size(); t++) {
+    solve_axis[t] = p.solves[t].is_col;
+    solve_index[t] = p.solves[t].idx;
+    solve_level[t] = p.level[t];
+  }
+  *nsolves = (uint32_t)p.solves.size();
+  *solved = p.solved ? 1 : 0;
+  return CEL_OK;
 }
 
 cel_status cel_debug_schedule_fuzz(cel_ctx* ctx, uint64_t seed, uint32_t max_us) {

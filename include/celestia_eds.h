@@ -243,6 +243,14 @@ cel_status cel_dev_repair(cel_ctx* ctx, void* d_eds, uint8_t* present, uint32_t 
  * off. Outcomes must not change: it checks that the schedule's cross-stream dependencies
  * are complete. */
 cel_status cel_debug_schedule_fuzz(cel_ctx* ctx, uint64_t seed, uint32_t max_us);
+/* Tests only, host-only (no device): the plan of the byzantine replay in rsmt2d's sweep
+ * order for a presence mask (2k*2k): for each solve in sequence its axis (0 row, 1 col),
+ * index and level (solves of one level run together on the device; a solve's level is
+ * one more than that of every earlier solve that filled a cell it reads). The outputs
+ * hold up to 4k entries (each axis is solved at most once); *solved = 1 if the sweeps
+ * complete the square. */
+cel_status cel_debug_repair_plan(const uint8_t* present, uint32_t k, int32_t* solve_axis, int32_t* solve_index,
+                                 int32_t* solve_level, uint32_t* nsolves, int32_t* solved);
 
 /* ------------------------------------------------------- exported trees, proofs
  * pkg/proof (proof.go:78-202, row_proof.go, share_proof.go) and the subtree-root
