@@ -1,0 +1,61 @@
+/*
+ * A plain C99 client of include/celestia_eds.h, the way the cgo stub (go/celestiaeds)
+ * binds it: compiled by gcc (not hipcc), linked against libcelestia_eds.so, no HIP or
+ * torch headers. It runs da.ExtendShares + NewDataAvailabilityHeader on the generateShares
+ * square of pkg/da/data_availability_header_test.go:247-263 (k = 2) and checks the DAH
+ * known answer of :45, then the DAH-only call shape (eds_out = NULL) and the
+ * "not a power of 2" error string of :68.
+ * Exit codes: 0 = all checks passed; 2 = no device (CEL_EDEVICE from cel_ctx_create:
+ * the library fails loudly, there is no CPU fallback); 1 = a check failed.
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "celestia_eds.h"
+
+static const char* kTypicalK2 = "b56e4d251ac266f4b91cc5464b3fc7efcbdc888064647496d13133f0dc65ac25";
+
+static void hex(const uint8_t* b, size_t n, char* out) {
+  for (size_t i = 0; i < n; i++) sprintf(out + 2 * i, "%02x", b[i]);
+}
+
+int main(void) {
+  cel_ctx* ctx = NULL;
+  cel_status st = cel_ctx_create(0, &ctx);
+  if (st == CEL_EDEVICE) {
+    printf("no device: %s\n", cel_strerror(st));
+    return 2;
+  }
+  if (st != CEL_OK) return 1;
+  enum { K = 2, N = K * K, W = 2 * K };
+  uint8_t* shares = (uint8_t*)malloc((size_t)N * CEL_SHARE_SIZE);
+  for (int i = 0; i < N; i++) {
+    uint8_t* s = shares + (size_t)i * CEL_SHARE_SIZE;
+    memset(s, 0xFF, CEL_SHARE_SIZE);
+    memset(s, 0, 19);       /* namespace version 0, 18 zero bytes */
+    memset(s + 19, 1, 10);  /* MustNewV0(0x01 * 10) */
+  }
+  uint8_t* eds = (uint8_t*)malloc((size_t)W * W * CEL_SHARE_SIZE);
+  uint8_t rr[W * CEL_NMT_NODE_SIZE], cr[W * CEL_NMT_NODE_SIZE], dah[32];
+  char h[65];
+  int ok = 1;
+  st = cel_extend_shares(ctx, shares, N, CEL_SHARE_SIZE, eds, rr, cr, dah, CEL_FLAG_ORDER_CHECK);
+  hex(dah, 32, h);
+  printf("ExtendShares: status %d dah %s\n", st, h);
+  ok &= st == CEL_OK && strcmp(h, kTypicalK2) == 0;
+  ok &= memcmp(eds, shares, CEL_SHARE_SIZE) == 0; /* cell (0,0) is the first share */
+  memset(dah, 0, sizeof dah);
+  st = cel_extend_shares(ctx, shares, N, CEL_SHARE_SIZE, NULL, rr, cr, dah, CEL_FLAG_ORDER_CHECK);
+  hex(dah, 32, h);
+  printf("DAH only:     status %d dah %s\n", st, h);
+  ok &= st == CEL_OK && strcmp(h, kTypicalK2) == 0;
+  st = cel_extend_shares(ctx, shares, 3, CEL_SHARE_SIZE, NULL, rr, cr, dah, 0);
+  printf("3 shares:     status %d \"%s\"\n", st, cel_last_error(ctx));
+  ok &= st == CEL_ENOTPOW2 && strcmp(cel_last_error(ctx), "number of shares is not a power of 2: got 3") == 0;
+  cel_ctx_destroy(ctx);
+  free(eds);
+  free(shares);
+  printf("%s\n", ok ? "ok" : "FAILED");
+  return ok ? 0 : 1;
+}
