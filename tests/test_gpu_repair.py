@@ -494,8 +494,8 @@ def test_repair_schedule_fuzz(ctx, oracle, k):
     masks = [(np.random.default_rng(s).random((w, w)) < p).astype(np.uint8)
              for s, p in ((1, 0.44), (2, 0.46), (25, 0.44))]
     try:
-        for fseed in range(3):
-            assert ctx.lib.cel_debug_schedule_fuzz(ctx.handle, 1000 + fseed, 60) == _lib.OK
+        for fseed in range(6):  # idle kernels of up to 60 us, then up to 250 us
+            assert ctx.lib.cel_debug_schedule_fuzz(ctx.handle, 1000 + fseed, 60 if fseed < 3 else 250) == _lib.OK
             for present in masks:
                 _, ok = _crossword_passes(present, k)
                 st, cells, _ = _dev_repair(ctx, eds, present, rr, cr)
