@@ -1309,8 +1309,8 @@ static SweepPlan plan_sweeps(const std::vector<uint8_t>& hm, uint32_t k) {
   return p;
 }
 
-static cel_status repair_exact(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>& hm, uint32_t k, const Verify& base,
-                               const RepairOut& out) {
+static cel_status repair_exact(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>& hm, uint32_t k,
+                               const uint8_t* row_roots, const uint8_t* col_roots, const RepairOut& out) {
   const Range range("repair.exact");
   const uint32_t W = 2 * k;
   const size_t cells = (size_t)W * W;
@@ -1318,85 +1318,122 @@ static cel_status repair_exact(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>
   const std::vector<Solve>& solves = plan.solves;
   const std::vector<int32_t>& level = plan.level;
   const std::vector<Check>& order = plan.order;
-  const int32_t nlevels = plan.nlevels;
-  const bool solved = plan.solved;
-  const auto& cnt = plan.cnt;
-  // device: the starting mask again, every level's axis lists in one upload (each axis is
-  // solved once: at most 2W entries), then the levels in order on the main stream. The
-  // register decoder takes a level's rows and columns in one launch (direction in bit 30
-  // of each entry); the LDS path gathers one direction per launch.
+  const size_t S = solves.size();
+  // order[first[t] .. first[t + 1]) = solve t's checks (SOLVE, then its ORTH axes)
+  std::vector<size_t> first(S + 1, order.size());
+  for (size_t o = 0; o < order.size(); o++)
+    if (order[o].kind == Check::SOLVE) first[(size_t)order[o].solve] = o;
   const bool in_square = rs_decode_axis_supported(W, kShare);
-  std::vector<int32_t> lists;
-  struct Group {
-    uint32_t off, n;
-    int is_col;  // -1: mixed
-  };
-  std::vector<Group> groups;
-  {
-    std::vector<std::vector<int32_t>> by[2];
-    by[0].resize(nlevels + 1);
-    by[1].resize(nlevels + 1);
-    for (size_t t = 0; t < solves.size(); t++) by[solves[t].is_col][level[t]].push_back(solves[t].idx);
-    for (int32_t L = 1; L <= nlevels; L++) {
-      if (in_square) {
-        const uint32_t off = (uint32_t)lists.size();
-        for (int d = 0; d < 2; d++)
-          for (int32_t i : by[d][L]) lists.push_back(d ? (int32_t)((uint32_t)i | (1u << 30)) : i);
-        if ((uint32_t)lists.size() > off) groups.push_back({off, (uint32_t)lists.size() - off, -1});
-        continue;
-      }
-      for (int d = 0; d < 2; d++)
-        if (!by[d][L].empty()) {
-          groups.push_back({(uint32_t)lists.size(), (uint32_t)by[d][L].size(), d});
-          lists.insert(lists.end(), by[d][L].begin(), by[d][L].end());
-        }
-    }
-  }
+  // roots of the checked axes: 96-byte records after the axes-roots workspace (b.work holds
+  // the whole-square commit's workspace, which is larger)
+  const size_t ws_axes = (axes_roots_workspace_size(k, W) + 255) & ~(size_t)255;
+  uint32_t* d_rec = reinterpret_cast<uint32_t*>(b.work + ws_axes);
+  std::vector<uint8_t> h_rec((size_t)2 * W * kNodeWords * 4);
+  std::vector<int32_t> h_flags((size_t)2 * W);
   hipError_t e;
   cel_status st;
-  // both streams are idle (verify_square synchronised the joined streams)
+  // both streams are idle (verify_square synchronised the joined streams); the square keeps
+  // the bytes of every cell known at the start (decoders store erased cells only)
   std::memcpy(b.hmask, hm.data(), cells);
-  std::memcpy(b.hidx, lists.data(), lists.size() * 4);
-  b.slot = (uint32_t)((lists.size() + W - 1) / W);  // the slots the lists occupy
   if ((e = hipMemcpyAsync(b.mask, b.hmask, cells, hipMemcpyHostToDevice, b.main)) != hipSuccess ||
-      (!lists.empty() && (e = hipMemcpyAsync(b.idx, b.hidx, lists.size() * 4, hipMemcpyHostToDevice, b.main)) != hipSuccess) ||
       (e = hipMemsetAsync(b.flags, 0, 2 * (size_t)W * 4, b.main)) != hipSuccess)
     return hip_fail(ctx, e, "H2D");
-  for (const Group& g : groups) {
-    const int32_t* idx = b.idx + g.off;
-    if ((st = fuzz(ctx, b.main)) != CEL_OK) return st;
-    if (in_square) {
-      e = launch_rs_decode_in_square(b.eds, b.mask, W, idx, g.is_col, g.n, ctx->tables.mul8, b.main);
-    } else if ((e = launch_gather_axes(b.eds, b.mask, W, idx, g.is_col, g.n, b.dense[0], b.dmask, b.main)) ==
-                   hipSuccess &&
-               (e = launch_rs_decode(b.dense[0], b.dmask, g.n, k, kShare, ctx->tables, nullptr, b.main)) ==
-                   hipSuccess) {
-      e = launch_scatter_axes(b.eds, b.mask, W, idx, g.is_col, g.n, b.dense[0], b.main);
+  // The sequence runs in prefixes of CH solves. A prefix's solves depend only on earlier
+  // solves, so each prefix runs level by level after the previous one; then its checks
+  // (encoding and root of every axis it solves or completes) come back, and the first
+  // failure in sweep order ends the replay there: rsmt2d returns at its first failing check.
+  const size_t CH = std::max<size_t>(16, W / 4);
+  for (size_t s0 = 0; s0 < S; s0 += CH) {
+    const size_t s1 = std::min(S, s0 + CH);
+    std::vector<int32_t> lists;
+    struct Group {
+      uint32_t off, n;
+      int is_col;  // -1: mixed (register decoder, direction in bit 30)
+    };
+    std::vector<Group> groups;
+    {
+      int32_t lo = INT32_MAX, hi = 0;
+      for (size_t t = s0; t < s1; t++) {
+        lo = std::min(lo, level[t]);
+        hi = std::max(hi, level[t]);
+      }
+      std::vector<std::vector<int32_t>> by[2];
+      by[0].resize((size_t)(hi - lo + 1));
+      by[1].resize((size_t)(hi - lo + 1));
+      for (size_t t = s0; t < s1; t++) by[solves[t].is_col][(size_t)(level[t] - lo)].push_back(solves[t].idx);
+      for (size_t L = 0; L < by[0].size(); L++) {
+        if (in_square) {
+          const uint32_t off = (uint32_t)lists.size();
+          for (int d = 0; d < 2; d++)
+            for (int32_t i : by[d][L]) lists.push_back(d ? (int32_t)((uint32_t)i | (1u << 30)) : i);
+          if ((uint32_t)lists.size() > off) groups.push_back({off, (uint32_t)lists.size() - off, -1});
+          continue;
+        }
+        for (int d = 0; d < 2; d++)
+          if (!by[d][L].empty()) {
+            groups.push_back({(uint32_t)lists.size(), (uint32_t)by[d][L].size(), d});
+            lists.insert(lists.end(), by[d][L].begin(), by[d][L].end());
+          }
+      }
     }
-    if (e != hipSuccess) return hip_fail(ctx, e, "solve");
-  }
-  // encoding checks of every axis complete at the end (the sanity axes passed already and
-  // pass again), on the side stream after the last level
-  if ((e = hipEventRecord(b.ev_main, b.main)) != hipSuccess || (e = hipStreamWaitEvent(b.side, b.ev_main, 0)) != hipSuccess)
-    return hip_fail(ctx, e, "event");
-  std::vector<int32_t> comp[2];
-  for (int d = 0; d < 2; d++)
-    for (uint32_t i = 0; i < W; i++)
-      if (cnt[d][i] == W) comp[d].push_back((int32_t)i);
-  if ((st = check_pass(ctx, b, k, 0, comp[0], false)) != CEL_OK) return st;
-  Verify v = base;
-  if ((st = verify_square(ctx, b, k, 1, comp[1], &v)) != CEL_OK) return st;
-  cel_status code;
-  const long f = v.first_failure(order, &code);
-  if (f >= 0) {
-    const Check& c = order[(size_t)f];
-    rollback(hm, W, solves, (size_t)c.solve);
-    return fail_axis(ctx, b, hm, out, code, c.is_col, c.idx, c.kind == Check::SOLVE);
+    // the axes this prefix's checks look at, by direction (each axis is checked once)
+    std::vector<int32_t> chk[2];
+    for (size_t o = first[s0]; o < first[s1]; o++) chk[order[o].is_col].push_back(order[o].idx);
+    const uint32_t off_chk0 = (uint32_t)lists.size();
+    lists.insert(lists.end(), chk[0].begin(), chk[0].end());
+    const uint32_t off_chk1 = (uint32_t)lists.size();
+    lists.insert(lists.end(), chk[1].begin(), chk[1].end());
+    std::memcpy(b.hidx, lists.data(), lists.size() * 4);
+    if ((e = hipMemcpyAsync(b.idx, b.hidx, lists.size() * 4, hipMemcpyHostToDevice, b.main)) != hipSuccess)
+      return hip_fail(ctx, e, "H2D");
+    for (const Group& g : groups) {
+      const int32_t* idx = b.idx + g.off;
+      if ((st = fuzz(ctx, b.main)) != CEL_OK) return st;
+      if (in_square) {
+        e = launch_rs_decode_in_square(b.eds, b.mask, W, idx, g.is_col, g.n, ctx->tables.mul8, b.main);
+      } else if ((e = launch_gather_axes(b.eds, b.mask, W, idx, g.is_col, g.n, b.dense[0], b.dmask, b.main)) ==
+                     hipSuccess &&
+                 (e = launch_rs_decode(b.dense[0], b.dmask, g.n, k, kShare, ctx->tables, nullptr, b.main)) ==
+                     hipSuccess) {
+        e = launch_scatter_axes(b.eds, b.mask, W, idx, g.is_col, g.n, b.dense[0], b.main);
+      }
+      if (e != hipSuccess) return hip_fail(ctx, e, "solve");
+    }
+    // encoding check and root of every checked axis, one direction at a time through dchk
+    for (int d = 0; d < 2; d++) {
+      const uint32_t na = (uint32_t)chk[d].size();
+      if (!na) continue;
+      const int32_t* idx = b.idx + (d ? off_chk1 : off_chk0);
+      uint32_t* rec = d_rec + (size_t)d * W * kNodeWords;
+      if ((e = launch_gather_axes(b.eds, b.mask, W, idx, d, na, b.dchk, b.dmask_chk, b.main)) != hipSuccess)
+        return hip_fail(ctx, e, "gather");
+      if ((st = encode_check(ctx, b, k, d, na, b.dchk, idx, b.main)) != CEL_OK) return st;
+      if ((e = launch_axes_roots(b.dchk, k, idx, na, rec, b.work, b.main)) != hipSuccess)
+        return hip_fail(ctx, e, "roots");
+    }
+    if ((e = hipMemcpyAsync(h_flags.data(), b.flags, h_flags.size() * 4, hipMemcpyDeviceToHost, b.main)) !=
+            hipSuccess ||
+        (e = hipMemcpyAsync(h_rec.data(), d_rec, h_rec.size(), hipMemcpyDeviceToHost, b.main)) != hipSuccess ||
+        (e = hipStreamSynchronize(b.main)) != hipSuccess)
+      return hip_fail(ctx, e, "D2H");
+    // replay the prefix's checks in sweep order
+    size_t pos[2] = {0, 0};
+    for (size_t o = first[s0]; o < first[s1]; o++) {
+      const Check& c = order[o];
+      const uint8_t* got = h_rec.data() + ((size_t)c.is_col * W + pos[c.is_col]++) * kNodeWords * 4;
+      const uint8_t* exp = (c.is_col ? col_roots : row_roots) + (size_t)c.idx * kNode;
+      const bool root_ok = std::memcmp(got, exp, kNode) == 0;
+      const bool enc_ok = h_flags[(size_t)c.is_col * W + (size_t)c.idx] == 0;
+      if (!root_ok || !enc_ok) {
+        rollback(hm, W, solves, (size_t)c.solve);
+        return fail_axis(ctx, b, hm, out, CEL_EBYZANTINE, c.is_col, c.idx, c.kind == Check::SOLVE);
+      }
+    }
   }
   // not reached for a square the pass schedule found byzantine (the outcome does not depend
   // on the order when every check passes), kept for completeness
-  if (!solved) {
-    rollback(hm, W, solves, solves.size());
+  if (!plan.solved) {
+    rollback(hm, W, solves, S);
     return fail(ctx, CEL_EUNREPAIRABLE, "failed to solve data square");
   }
   std::fill(hm.begin(), hm.end(), (uint8_t)1);
@@ -1523,7 +1560,7 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
   if (f >= 0) {
     const Check& c = order[(size_t)f];
     if (c.kind == Check::SANITY) return fail_axis(ctx, b, hm, out, code, c.is_col, c.idx, false);
-    return repair_exact(ctx, b, hm, k, v, out);
+    return repair_exact(ctx, b, hm, k, row_roots, col_roots, out);
   }
   if (!solved) {
     rollback(hm, W, solves, solves.size());
