@@ -48,3 +48,57 @@ def test_two_rank_processes_gloo(oracle, tmp_path):
         got = np.load(tmp_path / f"r{r}.npz")
         assert np.array_equal(got["rr"], rr) and np.array_equal(got["cr"], cr)
         assert got["dah"].tobytes() == dah
+
+
+def _rccl_one_rank(rank, port, k, outdir):
+    """One rank on a real RCCL communicator (the box has one GPU, and RCCL refuses two
+    ranks on one device: "Duplicate GPU detected", profiles/r3_rccl_probe.txt). Runs the
+    collectives TorchComm issues on device tensors of the shapes the sharded square
+    uses, then a whole n=1 square through TorchComm on the square's HIP stream."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    import torch
+    import torch.distributed as dist
+    from celestia_eds import default_context
+    from celestia_eds.sharded import RECORD, DeviceSteps, ShardedSquare, TorchComm
+    from celestia_eds.testfactory import random_ods
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    assert dist.get_backend() == "nccl"
+    comm = TorchComm()
+    steps = DeviceSteps(default_context(0), 0)
+    g = torch.Generator(device="cpu").manual_seed(5)
+    send = torch.randint(0, 256, (1, k, 2 * k, 512), dtype=torch.uint8, generator=g).to(dev)
+    recv = torch.empty_like(send)
+    rec = torch.randint(0, 256, (2 * k, RECORD), dtype=torch.uint8, generator=g).to(dev)
+    rec_all = torch.empty((1, 2 * k, RECORD), dtype=torch.uint8, device=dev)
+    st = torch.tensor([3], dtype=torch.int32, device=dev)
+    with steps.scope():
+        comm.all_to_all(recv.view(-1), send.view(-1))
+        comm.all_gather(rec_all.view(-1), rec.view(-1))
+        comm.all_reduce_max(st)
+    torch.cuda.synchronize()
+    ok = bool(torch.equal(recv, send) and torch.equal(rec_all[0], rec) and int(st.item()) == 3)
+    sq = ShardedSquare(k, 0, 1, steps)
+    sq.ods_rows.copy_(torch.from_numpy(np.ascontiguousarray(random_ods(k, 78))))
+    sq.run(comm)
+    torch.cuda.synchronize()
+    sq.check_status()
+    np.savez(os.path.join(outdir, "rccl.npz"), ok=ok, rr=sq.row_roots.cpu().numpy(),
+             cr=sq.col_roots.cpu().numpy(), dah=sq.dah.cpu().numpy())
+    dist.destroy_process_group()
+
+
+def test_rccl_one_rank_torchcomm(oracle, tmp_path):
+    import torch.multiprocessing as mp
+    from celestia_eds.testfactory import random_ods
+    k = 256
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_rccl_one_rank, args=(port, k, str(tmp_path)), nprocs=1, join=True)
+    got = np.load(tmp_path / "rccl.npz")
+    assert bool(got["ok"]), "RCCL collectives on device tensors returned wrong data"
+    _, rr, cr, dah = oracle.extend_and_commit(random_ods(k, 78), want_eds=False)
+    assert np.array_equal(got["rr"], rr) and np.array_equal(got["cr"], cr)
+    assert got["dah"].tobytes() == dah
