@@ -20,6 +20,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -937,6 +938,23 @@ static cel_status encode_check(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_c
   return CEL_OK;
 }
 
+// Encoding check of na complete axes of the square (list idx on the device) on stream s:
+// one in-place launch (k_rs_check_axes) for k = 32..128, else gather into dchk and
+// encode_check.
+static cel_status check_in_square(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_col, uint32_t na,
+                                  const int32_t* idx, hipStream_t s) {
+  const uint32_t W = 2 * k;
+  hipError_t e;
+  if (k >= 32 && k <= kMaxGf8Width) {
+    if ((e = launch_rs_check_axes(b.eds, k, idx, is_col, na, b.flags + (size_t)is_col * W, s)) != hipSuccess)
+      return hip_fail(ctx, e, "encoding check");
+    return CEL_OK;
+  }
+  if ((e = launch_gather_axes(b.eds, b.mask, W, idx, is_col, na, b.dchk, b.dmask_chk, s)) != hipSuccess)
+    return hip_fail(ctx, e, "gather");
+  return encode_check(ctx, b, k, is_col, na, b.dchk, idx, s);
+}
+
 // rsmt2d solveCrossword's decode of `list` (incomplete axes of one direction), in two
 // halves so the host can put other side-stream work between them:
 //   solve_issue  the decode on the main stream (in place in the square, or gather ->
@@ -978,7 +996,10 @@ static cel_status solve_issue(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_co
   return CEL_OK;
 }
 
-// The side half of a solve_issue; ev_main must still be that solve's record.
+// The side half of a solve_issue, enqueued after it with ev_main that solve's record or a
+// later one of the main stream (the axes it checks are final from their pass on). Dense
+// path: it must be enqueued before the solve after next, which reuses dense[s.d] once
+// this check has recorded ev_side[s.d].
 static cel_status solve_check(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_col, const Issued& s) {
   if (!s.na) return CEL_OK;
   const uint32_t W = 2 * k;
@@ -986,11 +1007,8 @@ static cel_status solve_check(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_co
   if ((e = hipStreamWaitEvent(b.side, b.ev_main, 0)) != hipSuccess) return hip_fail(ctx, e, "event");
   cel_status st;
   if ((st = fuzz(ctx, b.side)) != CEL_OK) return st;
-  if (rs_decode_axis_supported(W, kShare)) {  // the completed axes are gathered for their check
-    if ((e = launch_gather_axes(b.eds, b.mask, W, s.idx, is_col, s.na, b.dchk, b.dmask_chk, b.side)) != hipSuccess)
-      return hip_fail(ctx, e, "gather");
-    return encode_check(ctx, b, k, is_col, s.na, b.dchk, s.idx, b.side);
-  }
+  if (rs_decode_axis_supported(W, kShare))  // the completed axes are checked in the square
+    return check_in_square(ctx, b, k, is_col, s.na, s.idx, b.side);
   if ((st = encode_check(ctx, b, k, is_col, s.na, b.dense[s.d], s.idx, b.side)) != CEL_OK) return st;
   if ((e = hipEventRecord(b.ev_side[s.d], b.side)) != hipSuccess) return hip_fail(ctx, e, "event");
   return CEL_OK;
@@ -1003,7 +1021,7 @@ static cel_status solve_check(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_co
 static cel_status check_pass(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_col, const std::vector<int32_t>& list,
                              bool wait_main) {
   const Range range("repair.check");
-  const uint32_t W = 2 * k, na = (uint32_t)list.size();
+  const uint32_t na = (uint32_t)list.size();
   if (!na) return CEL_OK;
   hipError_t e;
   if (wait_main &&
@@ -1012,9 +1030,7 @@ static cel_status check_pass(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_col
   int32_t* idx;
   cel_status st;
   if ((st = upload_list(ctx, b, list, b.side, &idx)) != CEL_OK || (st = fuzz(ctx, b.side)) != CEL_OK) return st;
-  if ((e = launch_gather_axes(b.eds, b.mask, W, idx, is_col, na, b.dchk, b.dmask_chk, b.side)) != hipSuccess)
-    return hip_fail(ctx, e, "gather");
-  return encode_check(ctx, b, k, is_col, na, b.dchk, idx, b.side);
+  return check_in_square(ctx, b, k, is_col, na, idx, b.side);
 }
 
 // One check of the replay, in rsmt2d's order (oracle/eds.c orc_repair):
@@ -1209,19 +1225,29 @@ static cel_status fail_axis(cel_ctx* ctx, const RepairBufs& b, const std::vector
                              : std::string("byzantine ") + (is_col ? "column" : "row") + " " + std::to_string(idx));
 }
 
+#ifndef CEL_REPAIR_CHECKS_FIRST
+#define CEL_REPAIR_CHECKS_FIRST 1
+#endif
 // Commit every root of the square on the main stream beside the side stream's last checks,
 // join the streams and read roots and flags back (one page-locked copy).
-static cel_status verify_square(cel_ctx* ctx, RepairBufs& b, uint32_t k, int pending_col,
-                                const std::vector<int32_t>& pending, Verify* v) {
+static cel_status verify_square(cel_ctx* ctx, RepairBufs& b, uint32_t k, int last_col, const Issued& last,
+                                int pending_col, const std::vector<int32_t>& pending, Verify* v) {
   const uint32_t W = 2 * k;
   const size_t roots_b = (size_t)W * kNode;
   hipError_t e;
   cel_status st;
   if ((st = fuzz(ctx, b.main)) != CEL_OK) return st;
+  // the last pass's checks go to the side stream ahead of the commit's dozen launches, so
+  // they run beside its leaf hashing instead of trailing its tree levels
+  if (CEL_REPAIR_CHECKS_FIRST && ((st = solve_check(ctx, b, k, last_col, last)) != CEL_OK ||
+                                  (st = check_pass(ctx, b, k, pending_col, pending, false)) != CEL_OK))
+    return st;
   if ((e = launch_commit(b.eds, k, 1, b.roots, b.roots + roots_b, nullptr, nullptr, b.work, false, b.main)) !=
       hipSuccess)
     return hip_fail(ctx, e, "roots");
-  if ((st = check_pass(ctx, b, k, pending_col, pending, false)) != CEL_OK) return st;
+  if (!CEL_REPAIR_CHECKS_FIRST && ((st = solve_check(ctx, b, k, last_col, last)) != CEL_OK ||
+                                   (st = check_pass(ctx, b, k, pending_col, pending, false)) != CEL_OK))
+    return st;
   if ((e = hipEventRecord(b.ev_done, b.side)) != hipSuccess || (e = hipStreamWaitEvent(b.main, b.ev_done, 0)) != hipSuccess)
     return hip_fail(ctx, e, "join");
   if ((e = hipMemcpyAsync(b.hres, b.roots, b.res_bytes, hipMemcpyDeviceToHost, b.main)) != hipSuccess)
@@ -1474,18 +1500,27 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
   // The first row pass goes to the device before the host builds its bookkeeping (the
   // mask bitsets, the sanity lists), which then runs beside the decode.
   std::vector<int32_t> list, orth, first;
-  for (uint32_t i = 0; i < W; i++) {
+  for (uint32_t i = 0; i < W; i++) {  // hm bytes are 0 / 1: a word's popcount is its count
     const uint8_t* r = hm.data() + (size_t)i * W;
     uint32_t c = 0;
-    for (uint32_t j = 0; j < W; j++) c += r[j];
+    uint32_t j = 0;
+    for (; j + 8 <= W; j += 8) {
+      uint64_t x;
+      std::memcpy(&x, r + j, 8);
+      c += (uint32_t)__builtin_popcountll(x);
+    }
+    for (; j < W; j++) c += r[j];
     if (c >= k && c < W) first.push_back((int32_t)i);
   }
-  {
-    Issued s0;
-    if ((st = solve_issue(ctx, b, k, 0, first, &s0)) != CEL_OK || (st = solve_check(ctx, b, k, 0, s0)) != CEL_OK)
-      return st;
-  }
+  // Each pass's encoding check (side stream) is enqueued after the next pass's decode, so
+  // the host's enqueue of it is off the solve chain (the checked axes are final from their
+  // pass on; the dense path's buffer dense[d] is reused two passes later, after the check
+  // has recorded ev_side[d]).
+  Issued prev;
+  int prev_col = 0;
+  if ((st = solve_issue(ctx, b, k, 0, first, &prev)) != CEL_OK) return st;
   bool first_issued = !first.empty();
+  std::unique_ptr<Range> plan_range(new Range("repair.plan"));
   MaskBits mb(hm, W);
   std::vector<Check> order;
   std::vector<Solve> solves;
@@ -1506,6 +1541,7 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
   // them right after that pass's own encoding checks.
   std::vector<int32_t> pending;
   int pending_col = 0;
+  plan_range.reset();
   // passes: all solvable rows, then all solvable columns, until solved or stuck
   bool solved = false;
   std::vector<std::vector<int32_t>> by_solve;
@@ -1524,13 +1560,16 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
       } else {
         Issued s1;
         if ((st = solve_issue(ctx, b, k, is_col, list, &s1)) != CEL_OK ||
-            (st = check_pass(ctx, b, k, pending_col, pending, false)) != CEL_OK ||
-            (st = solve_check(ctx, b, k, is_col, s1)) != CEL_OK)
+            (st = solve_check(ctx, b, k, prev_col, prev)) != CEL_OK ||
+            (st = check_pass(ctx, b, k, pending_col, pending, false)) != CEL_OK)
           return st;
+        prev = s1;
+        prev_col = is_col;
         pending.clear();
       }
       // sequential view of the pass: solve i fills its missing cells, completing the
       // orthogonal axes whose last missing cell it held
+      const Range fill_range("repair.fill");
       mb.fill_pass(is_col, list, by_solve);
       for (size_t t = 0; t < list.size(); t++) {
         const int32_t si = (int32_t)solves.size();
@@ -1554,7 +1593,7 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
     if (!progress) break;
   }
   Verify v{nullptr, nullptr, row_roots, col_roots, W};
-  if ((st = verify_square(ctx, b, k, pending_col, pending, &v)) != CEL_OK) return st;
+  if ((st = verify_square(ctx, b, k, prev_col, prev, pending_col, pending, &v)) != CEL_OK) return st;
   cel_status code;
   const long f = v.first_failure(order, &code);
   if (f >= 0) {

@@ -79,6 +79,10 @@ void free_tables(DeviceTables* t);
 hipError_t launch_rs_encode(const RsGeom& g, const DeviceTables& t, hipStream_t s);
 hipError_t launch_rs_encode_bitslice(const RsGeom& g, hipStream_t s);  // GF(2^8), n <= 16
 hipError_t launch_rs_encode_axis(const RsGeom& g, hipStream_t s);       // GF(2^8), 32 <= n <= 128
+// Encoding check of listed axes in place in a resident EDS (flags[axis] |= 1 on mismatch),
+// GF(2^8), k = 32, 64, 128.
+hipError_t launch_rs_check_axes(const uint8_t* eds, uint32_t k, const int32_t* idx, int is_col, uint32_t naxes,
+                                int32_t* flags, hipStream_t s);
 hipError_t launch_rs_encode_gf16x(const RsGeom& g, hipStream_t s);     // GF(2^16), n = 256 / 512
 // Full 2D extension of nsq squares: Q0 rows -> Q1, then all 2k columns -> Q2|Q3.
 // ods == nullptr means Q0 is already in place inside eds.

@@ -194,6 +194,36 @@ hipError_t launch(const RsGeom& g, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Encoding check of listed axes of a resident EDS (rsmt2d verifyEncoding after a solve,
+// and the sanity / orthogonal checks): tile = (listed axis a, 256-byte slice y), one wave.
+// The data half (cells 0..K-1 of the axis) is encoded in registers as above and compared
+// with the parity half (cells K..2K-1) as it is loaded; a mismatch sets flags[axis]. One
+// launch in place of gather -> encode -> compare (no dense copy, no parity scratch).
+template <int LOGK>
+__global__ __launch_bounds__(256, 3) void k_rs_check_axes(const uint8_t* __restrict__ eds, uint32_t W,
+                                                          const int32_t* __restrict__ idx, int is_col, uint32_t naxes,
+                                                          int32_t* __restrict__ flags) {
+  constexpr int K = 1 << LOGK;
+  constexpr uint32_t nslice = kShare / 256;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t tile = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+  if (tile >= naxes * nslice) return;
+  const uint32_t y = tile % nslice, a = tile / nslice;
+  const uint32_t ax = (uint32_t)__builtin_amdgcn_readfirstlane(idx[a]);
+  const uint64_t base = is_col ? (uint64_t)ax * kShare : (uint64_t)ax * W * kShare;
+  const uint32_t stride = is_col ? W * kShare : kShare;
+  const auto rin = rsrc(eds + base + (uint64_t)y * 256u);
+  const uint32_t lo = lane * 4u;
+  uint32_t w[K];
+#pragma unroll
+  for (int i = 0; i < K; i++) w[i] = __builtin_amdgcn_raw_buffer_load_b32(rin, lo, (uint32_t)i * stride, 0);
+  transform_hyb<K>(w);
+  uint32_t diff = 0;
+#pragma unroll
+  for (int i = 0; i < K; i++) diff |= w[i] ^ __builtin_amdgcn_raw_buffer_load_b32(rin, lo, (uint32_t)(K + i) * stride, 0);
+  if (__any(diff != 0u) && lane == 0) atomicOr(flags + ax, 1);
+}
+
 }  // namespace ax
 
 // Byte offsets must fit the 32-bit buffer offsets: (n - 1) * shard stride + len < 2 GiB.
@@ -212,5 +242,19 @@ hipError_t launch_rs_encode_axis(const RsGeom& g, hipStream_t s) {
   }
 }
 
-}  // namespace cel
+hipError_t launch_rs_check_axes(const uint8_t* eds, uint32_t k, const int32_t* idx, int is_col, uint32_t naxes,
+                                int32_t* flags, hipStream_t s) {
+  const uint32_t W = 2 * k;
+  if ((uint64_t)(W - 1) * W * kShare + kShare >= 0x7fffffffull) return hipErrorInvalidValue;
+  if (naxes == 0) return hipSuccess;
+  const dim3 grid((naxes * (kShare / 256) + 3) / 4);
+  switch (k) {
+    case 32: hipLaunchKernelGGL(ax::k_rs_check_axes<5>, grid, dim3(256), 0, s, eds, W, idx, is_col, naxes, flags); break;
+    case 64: hipLaunchKernelGGL(ax::k_rs_check_axes<6>, grid, dim3(256), 0, s, eds, W, idx, is_col, naxes, flags); break;
+    case 128: hipLaunchKernelGGL(ax::k_rs_check_axes<7>, grid, dim3(256), 0, s, eds, W, idx, is_col, naxes, flags); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
 
+}  // namespace cel
