@@ -3,6 +3,8 @@
 - DAH known answers: pkg/da/data_availability_header_test.go:15-68
 - mainnet block 408 data root: x/blob/test/testdata/block_response.json (GF(2^8) pin)
 - Leopard table debug values and model digests: SURVEY.md Appendix A.2, A.3, A.5
+- Leopard = Lagrange RS over Cantor-basis points (tests/lagrange_rs.py): pinned on block
+  408 at GF(2^8), then equal to the oracle at k=128 and in GF(2^16) (k=256/512)
 - scalar vs SIMD oracle paths, decode round trips, repair semantics
 """
 import hashlib
@@ -75,6 +77,46 @@ def test_block408_data_root(oracle, golden, block408_ods):
     assert hashlib.sha256(eds.tobytes()).hexdigest() == g["eds_sha256"]
     assert rr[0].tobytes().hex() == g["row_root_0"] and cr[0].tobytes().hex() == g["col_root_0"]
     assert rr[-1].tobytes().hex() == g["row_root_last"] and cr[-1].tobytes().hex() == g["col_root_last"]
+
+
+def test_lagrange_rs_is_block408_code(oracle, golden, block408_ods):
+    """Leopard GF(2^8) = Lagrange RS over Cantor points (tests/lagrange_rs.py), on mainnet
+    block 408: Q1 of rows 0, 17 and Q2 of column 5 of the EDS whose sha256 the golden
+    fixture pins, at three byte positions each."""
+    import lagrange_rs as L
+    eds = oracle.extend(block408_ods)
+    assert hashlib.sha256(eds.tobytes()).hexdigest() == golden["block408"]["eds_sha256"]
+    f, k = L.Field(8, L.POLY8, L.CANTOR8), 32
+    for axis in (eds[0], eds[17], eds[:, 5]):
+        for b in (0, 200, 511):
+            assert L.encode(f, [int(v) for v in axis[:k, b]]) == [int(v) for v in axis[k:, b]]
+
+
+@pytest.mark.parametrize("m", [256, 512])
+def test_lagrange_rs_equals_gf16_oracle(oracle, m):
+    """GF(2^16), where the reference holds no vector: the oracle's FFT encoder equals the
+    same Lagrange statement (pinned at GF(2^8) above) with klauspost's GF(2^16) POLY and
+    Cantor basis; symbols are sym[j] = b[j] | b[j + 32] << 8 per 64-byte block."""
+    import lagrange_rs as L
+    f = L.Field(16, L.POLY16, L.CANTOR16)
+    for i in range(1, 16):  # the basis satisfies beta_i^2 + beta_i = beta_{i-1}
+        bi = L.CANTOR16[i]
+        assert f.mul(bi, bi) ^ bi == L.CANTOR16[i - 1]
+    data = np.random.default_rng(m).integers(0, 256, (m, 128), np.uint8)
+    par = oracle.rs_encode(data)
+    for blk, j in ((0, 0), (0, 31), (1, 9)):
+        sym = lambda a: [int(a[i, 64 * blk + j]) | int(a[i, 64 * blk + 32 + j]) << 8 for i in range(m)]
+        assert L.encode(f, sym(data)) == sym(par)
+
+
+def test_lagrange_rs_equals_gf8_oracle_k128(oracle):
+    """The k=128 code (256 shards, the last GF(2^8) width; block 408 is k=32)."""
+    import lagrange_rs as L
+    f, m = L.Field(8, L.POLY8, L.CANTOR8), 128
+    data = np.random.default_rng(128).integers(0, 256, (m, 64), np.uint8)
+    par = oracle.rs_encode(data)
+    for j in (0, 33, 63):
+        assert L.encode(f, [int(v) for v in data[:, j]]) == [int(v) for v in par[:, j]]
 
 
 def test_q3_both_ways(oracle):
