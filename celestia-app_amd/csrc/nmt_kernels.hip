@@ -385,7 +385,7 @@ __device__ __forceinline__ void sha_empty(uint32_t (&st)[8]) {
 
 // One workgroup per item list: items[g][n] 96-byte records -> 32-byte root (BE words in
 // out[g*8..]). Also packs the first n items into 90-byte outputs (row/col roots) if given.
-__global__ __launch_bounds__(256) void k_merkle(const uint32_t* __restrict__ items, const uint32_t* __restrict__ leafd,
+__global__ __launch_bounds__(1024) void k_merkle(const uint32_t* __restrict__ items, const uint32_t* __restrict__ leafd,
                                                 uint32_t n, uint8_t* __restrict__ dah, uint8_t* __restrict__ row_out,
                                                 uint8_t* __restrict__ col_out, const int32_t* __restrict__ bad_axis,
                                                 int32_t* __restrict__ status) {
@@ -447,6 +447,32 @@ __global__ __launch_bounds__(256) void k_merkle(const uint32_t* __restrict__ ite
     }
     if (status) status[g] = (bad_axis && bad_axis[g] != INT_MAX) ? CEL_EORDER : CEL_OK;
   }
+}
+
+// Threads of a k_merkle workgroup: one per pair of the widest level (each level is one
+// round of 2-compression hashes then), 64..1024.
+static uint32_t merkle_block(uint32_t n) {
+  const uint32_t pairs = ((n / 2 + 63) / 64) * 64;
+  return pairs < 64 ? 64u : (pairs > 1024 ? 1024u : pairs);
+}
+
+// RFC-6962 leaf digests of n node records, one lane each (k_merkle then starts from them),
+// and the records packed to 90 bytes: the first n/2 into row_out, the rest into col_out.
+__global__ __launch_bounds__(256) void k_dah_leaves(const uint32_t* __restrict__ items, uint32_t n,
+                                                    uint32_t* __restrict__ leafd, uint8_t* __restrict__ row_out,
+                                                    uint8_t* __restrict__ col_out) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  uint32_t R[kNodeWords], st[8];
+  load_node(items + (uint64_t)i * kNodeWords, R);
+  rfc_leaf90(R, st);
+  uint4* d = reinterpret_cast<uint4*>(leafd + (uint64_t)i * 8);
+  d[0] = make_uint4(st[0], st[1], st[2], st[3]);
+  d[1] = make_uint4(st[4], st[5], st[6], st[7]);
+  const uint32_t half = n / 2;
+  uint16_t* r16 = reinterpret_cast<uint16_t*>(i < half ? row_out + (uint64_t)i * kNode : col_out + (uint64_t)(i - half) * kNode);
+#pragma unroll
+  for (int j = 0; j < 45; j++) r16[j] = (uint16_t)(R[j / 2] >> (16 * (j & 1)));
 }
 
 __global__ void k_fill_i32(int32_t* p, uint32_t n, int32_t v) {
@@ -519,7 +545,8 @@ hipError_t launch_commit(const uint8_t* eds, uint32_t k, uint32_t nsq, uint8_t* 
   // roots already packed into row_roots / col_roots by the root level
   const Range r("dah");
   if (dah)
-    hipLaunchKernelGGL(k_merkle, dim3(nsq), dim3(256), lds, s, roots, leafd, trees, dah, nullptr, nullptr, bad, status);
+    hipLaunchKernelGGL(k_merkle, dim3(nsq), dim3(merkle_block(trees)), lds, s, roots, leafd, trees, dah, nullptr,
+                       nullptr, bad, status);
   return hipGetLastError();
 }
 
@@ -564,6 +591,32 @@ __global__ CEL_LEVEL_BOUNDS void k_level_grid(const uint32_t* __restrict__ in, u
   load_node(in + ri * kNodeWords, R);
   hash_node(L, R, o);
   store_node(out + (uint64_t)idx * kNodeWords, o);
+}
+
+// One level of two independent tree sets in one launch (the slab's column trees and row
+// subtrees): job j reduces trees_j trees of nin_j nodes, tree t's node l at
+// in_j[t * tstride_j + l * lstride_j], into out_j[t][nin_j / 2] (compact).
+struct LevelJob {
+  const uint32_t* in;
+  uint32_t* out;
+  uint32_t nin, trees, tstride, lstride;
+};
+
+__global__ CEL_LEVEL_BOUNDS void k_level_pair(LevelJob a, LevelJob b) {
+  uint32_t idx = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t na = a.nin > 1 ? a.trees * (a.nin / 2) : 0u;
+  const uint32_t nb = b.nin > 1 ? b.trees * (b.nin / 2) : 0u;
+  if (idx >= na + nb) return;
+  const LevelJob& j = idx < na ? a : b;
+  if (idx >= na) idx -= na;
+  const uint32_t nout = j.nin / 2;
+  const uint32_t t = idx / nout, l = idx % nout;
+  const uint64_t li = (uint64_t)t * j.tstride + (uint64_t)(2 * l) * j.lstride, ri = li + j.lstride;
+  uint32_t L[kNodeWords], R[kNodeWords], o[kNodeWords];
+  load_node(j.in + li * kNodeWords, L);
+  load_node(j.in + ri * kNodeWords, R);
+  hash_node(L, R, o);
+  store_node(j.out + (uint64_t)idx * kNodeWords, o);
 }
 
 // Push order across slab boundaries (rows of Q0): the last leaf of slab r-1 must not
@@ -620,10 +673,40 @@ static void reduce_grid(const uint32_t* in, uint32_t nin, uint32_t trees, uint32
   }
 }
 
-// Workspace: leaves [2k*w] | ping [k*w] | pong [k*w] | bad int32
+// Two tree sets reduced level by level in lockstep, one k_level_pair launch per level:
+// set j has trees_j trees of nin_j leaves (first level strided as in k_level_grid, then
+// compact in its own ping / pong buffers); each set's last level writes roots_j.
+static void reduce_grid_pair(LevelJob a, uint32_t* ping_a, uint32_t* pong_a, uint32_t* roots_a, LevelJob b,
+                             uint32_t* ping_b, uint32_t* pong_b, uint32_t* roots_b, hipStream_t s) {
+  uint32_t* dst_a = ping_a;
+  uint32_t* dst_b = ping_b;
+  while (a.nin > 1 || b.nin > 1) {
+    if (a.nin > 1) a.out = a.nin == 2 ? roots_a : dst_a;
+    if (b.nin > 1) b.out = b.nin == 2 ? roots_b : dst_b;
+    const uint32_t n = (a.nin > 1 ? a.trees * (a.nin / 2) : 0u) + (b.nin > 1 ? b.trees * (b.nin / 2) : 0u);
+    hipLaunchKernelGGL(k_level_pair, dim3((n + 255) / 256), dim3(256), 0, s, a, b);
+    if (a.nin > 1) {
+      a.in = a.out;
+      a.nin /= 2;
+      a.tstride = a.nin;
+      a.lstride = 1;
+      dst_a = dst_a == ping_a ? pong_a : ping_a;
+    }
+    if (b.nin > 1) {
+      b.in = b.out;
+      b.nin /= 2;
+      b.tstride = b.nin;
+      b.lstride = 1;
+      dst_b = dst_b == ping_b ? pong_b : ping_b;
+    }
+  }
+}
+
+// Workspace: leaves [2k*w] | ping, pong of the column trees [k*w] | roots area (unused) |
+//            bad int32 | ping, pong of the row subtrees [k*w]
 size_t slab_workspace_size(uint32_t k, uint32_t w) {
   const size_t nb = kNodeWords * 4, W = 2 * (size_t)k;
-  return align256(W * w * nb) + 2 * align256((size_t)k * w * nb + nb) + align256(W * 2 * nb) + 256;
+  return align256(W * w * nb) + 4 * align256((size_t)k * w * nb + nb) + align256(W * 2 * nb) + 256;
 }
 
 hipError_t launch_slab_commit(const uint8_t* slab, uint32_t k, uint32_t c0, uint32_t w, uint32_t* col_rec,
@@ -639,24 +722,29 @@ hipError_t launch_slab_commit(const uint8_t* slab, uint32_t k, uint32_t c0, uint
   base += align256((size_t)k * w * nb + nb);
   base += align256((size_t)W * 2 * nb);
   int32_t* bad = reinterpret_cast<int32_t*>(base);
+  base += 256;
+  uint32_t* ping2 = reinterpret_cast<uint32_t*>(base);
+  base += align256((size_t)k * w * nb + nb);
+  uint32_t* pong2 = reinterpret_cast<uint32_t*>(base);
   hipLaunchKernelGGL(k_fill_i32, dim3(1), dim3(64), 0, s, bad, 1u, INT_MAX);
   hipLaunchKernelGGL(k_fill_i32, dim3(1), dim3(64), 0, s, status, 1u, 0);
   dim3 gl((W * w + 255) / 256);
   if (order_check) hipLaunchKernelGGL(k_slab_leaf<true>, gl, dim3(256), 0, s, slab, k, c0, w, leaves, bad);
   else hipLaunchKernelGGL(k_slab_leaf<false>, gl, dim3(256), 0, s, slab, k, c0, w, leaves, bad);
-  // w column trees of 2k leaves (leaf i of column j at i*w + j)
-  reduce_grid(leaves, W, w, 1, w, ping, pong, col_rec, s);
-  // 2k row subtrees of w leaves (leaf j of row i at i*w + j)
+  // w column trees of 2k leaves (leaf i of column j at i*w + j) and 2k row subtrees of w
+  // leaves (leaf j of row i at i*w + j), both sets one level per launch
   if (w == 1) (void)hipMemcpyAsync(row_sub, leaves, (size_t)W * nb, hipMemcpyDeviceToDevice, s);
-  else reduce_grid(leaves, w, W, w, 1, ping, pong, row_sub, s);
+  const LevelJob cols{leaves, nullptr, W, w, 1, w};
+  const LevelJob rows{leaves, nullptr, w, W, w, 1};
+  reduce_grid_pair(cols, ping, pong, col_rec, rows, ping2, pong2, row_sub, s);
   hipLaunchKernelGGL(k_status_from_bad, dim3(1), dim3(64), 0, s, bad, status);
   return hipGetLastError();
 }
 
-// Workspace: ping/pong [2k * nranks / 2] | items [4k] | leafd unused | bad
+// Workspace: ping/pong [2k * nranks / 2] | items [4k] | bad | DAH leaf digests [4k][8]
 size_t shard_finish_workspace_size(uint32_t k, uint32_t nranks) {
   const size_t nb = kNodeWords * 4, W = 2 * (size_t)k;
-  return 2 * align256(W * (nranks / 2 + 1) * nb) + align256(2 * W * nb) + 256;
+  return 2 * align256(W * (nranks / 2 + 1) * nb) + align256(2 * W * nb) + 256 + align256(2 * W * 32);
 }
 
 hipError_t launch_shard_finish(const uint32_t* row_subs, const uint32_t* col_rec, uint32_t k, uint32_t nranks,
@@ -672,6 +760,8 @@ hipError_t launch_shard_finish(const uint32_t* row_subs, const uint32_t* col_rec
   uint32_t* items = reinterpret_cast<uint32_t*>(base);  // [rows 2k | cols 2k]
   base += align256((size_t)2 * W * nb);
   int32_t* bad = reinterpret_cast<int32_t*>(base);
+  base += 256;
+  uint32_t* leafd = reinterpret_cast<uint32_t*>(base);
   hipLaunchKernelGGL(k_fill_i32, dim3(1), dim3(64), 0, s, bad, 1u, INT_MAX);
   if (order_check && nranks > 1)
     hipLaunchKernelGGL(k_slab_boundary, dim3((k + 255) / 256), dim3(256), 0, s, row_subs, k, w, nranks, bad);
@@ -681,8 +771,12 @@ hipError_t launch_shard_finish(const uint32_t* row_subs, const uint32_t* col_rec
   (void)hipMemcpyAsync(items + (size_t)W * kNodeWords, col_rec, (size_t)W * nb, hipMemcpyDeviceToDevice, s);
   // previous status (all-reduced over ranks by the caller) survives; boundary adds to it
   hipLaunchKernelGGL(k_status_from_bad, dim3(1), dim3(64), 0, s, bad, status);
+  // the 4k RFC-6962 leaf digests and the packed roots one lane each, then the DAH tree
+  // one level per round in one workgroup
+  hipLaunchKernelGGL(k_dah_leaves, dim3((2 * W + 255) / 256), dim3(256), 0, s, items, 2 * W, leafd, row_roots,
+                     col_roots);
   const size_t lds = (size_t)2 * W * 8 * 4;
-  hipLaunchKernelGGL(k_merkle, dim3(1), dim3(256), lds, s, items, nullptr, 2 * W, dah, row_roots, col_roots,
+  hipLaunchKernelGGL(k_merkle, dim3(1), dim3(merkle_block(2 * W)), lds, s, items, leafd, 2 * W, dah, nullptr, nullptr,
                      nullptr, nullptr);
   return hipGetLastError();
 }
@@ -904,7 +998,8 @@ hipError_t launch_merkle_root(const uint8_t* items, uint32_t n, uint32_t item_le
   if (n) hipLaunchKernelGGL(k_pad_items, dim3((n + 255) / 256), dim3(256), 0, s, items, n, item_len, pad);
   const size_t lds = (size_t)(n ? n : 1) * 8 * 4;
   if (lds > 64 * 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_merkle, dim3(1), dim3(256), lds, s, pad, nullptr, n, out, nullptr, nullptr, nullptr, nullptr);
+  hipLaunchKernelGGL(k_merkle, dim3(1), dim3(merkle_block(n)), lds, s, pad, nullptr, n, out, nullptr, nullptr, nullptr,
+                     nullptr);
   return hipGetLastError();
 }
 
