@@ -203,7 +203,7 @@ def run_sharded(a):
     """Config 3: one k x k square per step, row-sharded over all ranks (strong scaling).
     Rank r row-encodes k/N rows straight into the all-to-all layout, one RCCL
     all_to_all_single transposes them into column slabs, each rank column-encodes and
-    hashes its slab, two all-gathers of 96-byte records and a combine give the roots
+    hashes its slab, one all-gather of 96-byte records and a combine give the roots
     and the DAH on every rank. At N = 1 the same schedule runs without collectives."""
     world, rank, local = _dist_env()
     local = _rank_device(local)
@@ -286,7 +286,7 @@ def run_sharded(a):
             "share_size": 512,
             "field": "GF(2^16)",
             "parallelism": f"rowshard{world}",
-            "collectives": "all_to_all_single (data), all_gather x2 + all_reduce (records)" if world > 1
+            "collectives": "all_to_all_single (data), one all_gather (records)" if world > 1
             else "none (N=1)",
         },
         "roofline": {
@@ -571,7 +571,7 @@ def _rowshard_fields(k, world, elapsed, steps, t_a2a):
     alone next to SURVEY §8e's one-link estimate (bytes per peer / 153 GB/s)."""
     per_peer = 2 * k * k * 512 // (world * world)  # (k/N rows) x (2k/N columns) x 512 B
     return {"workload": f"config 3: one k={k} square row-sharded over {world} GPU(s), one all_to_all_single "
-                        "(column slabs) + two record all_gathers",
+                        "(column slabs) + one record all_gather",
             "value": steps / elapsed, "unit": "squares/s", "n_gpus": world, "steps": steps,
             "ms_per_step": elapsed / steps * 1e3, "scaling": "strong",
             "a2a_us": t_a2a * 1e6 if world > 1 else None,

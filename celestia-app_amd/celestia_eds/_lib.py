@@ -86,7 +86,7 @@ def load():
             "cel_dev_shard_workspace_size": (sz, [u32, u32]),
             "cel_dev_shard_rows": (i32, [P, P, u32, u32, P, P]),
             "cel_dev_shard_cols": (i32, [P, P, u32, u32, u32, P, P, P, P, P, u32]),
-            "cel_dev_shard_finish": (i32, [P, P, P, u32, u32, P, P, P, P, P, P, u32]),
+            "cel_dev_shard_finish": (i32, [P, P, u32, u32, P, P, P, P, P, P, u32]),
             "cel_square_construct": (i32, [P, P, u32, u32, u32, u32, P, u32, P, P]),
             "cel_square_last_error": (ctypes.c_char_p, []),
             "cel_square_tx_range": (i32, [P, P, u32, u32, u32, u32, P, P]),

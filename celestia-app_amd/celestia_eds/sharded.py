@@ -9,15 +9,15 @@ all-to-all transpose, EDS columns [r*w, (r+1)*w) with w = 2k/N:
              (rows 0..k-1) of this rank's column slab [2k][w][512]
   3. cols    column-encode the slab (rows k..2k-1), hash its leaves once, build its
              w column trees and the 2k row subtrees over its w columns
-  4. gather  all_gather the row-subtree records and the column-root records, and a
-             max all_reduce of the push-order status
+  4. gather  one all_gather of each rank's record block [2k + w + 1][96]: its row
+             subtrees, its column roots and its push-order status
   5. finish  combine the N subtree roots of every row (log2 N levels of HashNode),
              then DataAvailabilityHeader.Hash over rowRoots || colRoots
 
 The result is what da.ExtendShares + da.NewDataAvailabilityHeader
 (pkg/da/data_availability_header.go:65-75, :44-63) give for the whole square. The
-only data-path collective is the all-to-all (2k*k*512/N^2 bytes per peer); the
-gathers move 96-byte records. `steps` does the per-rank device work (DeviceSteps:
+only data-path collective is the all-to-all (2k*k*512/N^2 bytes per peer); the one
+gather moves 96-byte records. `steps` does the per-rank device work (DeviceSteps:
 the C ABI cel_dev_shard_*); `comm` the collectives (TorchComm: torch.distributed,
 i.e. RCCL over xGMI on the GPU box, gloo in the CPU tests).
 """
@@ -45,9 +45,6 @@ class TorchComm:
     def all_gather(self, out, inp):
         self.dist.all_gather_into_tensor(out, inp, group=self.group)
 
-    def all_reduce_max(self, t):
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
-
 
 class StagedComm:
     """The same collectives over gloo on host copies of device tensors (gloo has no
@@ -68,11 +65,6 @@ class StagedComm:
         h_out = out.cpu()
         self.dist.all_gather_into_tensor(h_out, inp.cpu(), group=self.group)
         out.copy_(h_out)
-
-    def all_reduce_max(self, t):
-        h = t.cpu()
-        self.dist.all_reduce(h, op=self.dist.ReduceOp.MAX, group=self.group)
-        t.copy_(h)
 
 
 class DeviceSteps:
@@ -118,11 +110,11 @@ class DeviceSteps:
         c.check(c.lib.cel_dev_shard_cols(c.handle, self._p(slab), k, n, rank, self._p(col_rec), self._p(row_sub),
                                          self._p(status), self._p(self.work(k, n)), self._stream(), self.flags))
 
-    def finish(self, row_sub_all, col_rec_all, k, n, row_roots, col_roots, dah, status):
+    def finish(self, gathered, k, n, row_roots, col_roots, dah, status):
         c = self.ctx
-        c.check(c.lib.cel_dev_shard_finish(c.handle, self._p(row_sub_all), self._p(col_rec_all), k, n,
-                                           self._p(row_roots), self._p(col_roots), self._p(dah), self._p(status),
-                                           self._p(self.work(k, n)), self._stream(), self.flags))
+        c.check(c.lib.cel_dev_shard_finish(c.handle, self._p(gathered), k, n, self._p(row_roots), self._p(col_roots),
+                                           self._p(dah), self._p(status), self._p(self.work(k, n)), self._stream(),
+                                           self.flags))
 
 
 class ShardedSquare:
@@ -142,11 +134,15 @@ class ShardedSquare:
         # one rank: the all-to-all is the identity, so the row pass writes the slab's top
         # half directly (no 2k x k-cell copy)
         self.send = self.slab[:k].view(1, k, W, S) if n == 1 else e((n, self.rows_per_rank, self.w, S), u8)
-        self.col_rec = e((self.w, RECORD), u8)
-        self.row_sub = e((W, RECORD), u8)
-        self.row_sub_all = e((n, W, RECORD), u8)
-        self.col_rec_all = e((W, RECORD), u8)
-        self.status = e((1,), i32)
+        # this rank's record block, the all-gather's send buffer: row subtrees, column
+        # roots, then a record whose first int32 is the step-2 status
+        S = W + self.w + 1
+        self.pack = e((S, RECORD), u8)
+        self.row_sub = self.pack[:W]
+        self.col_rec = self.pack[W:W + self.w]
+        self.status_rec = self.pack[W + self.w].view(i32)[:1]
+        self.gathered = e((n, S, RECORD), u8)
+        self.status = e((1,), i32)  # the finish's: max over ranks, or EORDER across slabs
         self.row_roots = e((W, _lib.NMT_NODE_SIZE), u8)
         self.col_roots = e((W, _lib.NMT_NODE_SIZE), u8)
         self.dah = e((32,), u8)
@@ -165,16 +161,13 @@ class ShardedSquare:
         comm.all_to_all(top.view(-1), self.send.view(-1))
 
     def phase_cols(self):
-        self.steps.cols(self.slab, self.k, self.n, self.rank, self.col_rec, self.row_sub, self.status)
+        self.steps.cols(self.slab, self.k, self.n, self.rank, self.col_rec, self.row_sub, self.status_rec)
 
     def gather(self, comm):
-        comm.all_gather(self.row_sub_all.view(-1), self.row_sub.view(-1))
-        comm.all_gather(self.col_rec_all.view(-1), self.col_rec.view(-1))
-        comm.all_reduce_max(self.status)
+        comm.all_gather(self.gathered.view(-1), self.pack.view(-1))
 
     def phase_finish(self):
-        self.steps.finish(self.row_sub_all, self.col_rec_all, self.k, self.n, self.row_roots, self.col_roots,
-                          self.dah, self.status)
+        self.steps.finish(self.gathered, self.k, self.n, self.row_roots, self.col_roots, self.dah, self.status)
 
     def scope(self):
         sc = getattr(self.steps, "scope", None)
@@ -218,12 +211,8 @@ class LocalComm:
                     top[r].copy_(src.send[h])
         for s in squares:
             s.phase_cols()
-        row_sub_all = torch.stack([s.row_sub for s in squares])
-        col_rec_all = torch.cat([s.col_rec for s in squares])
-        status = torch.stack([s.status for s in squares]).max().reshape(1)
+        gathered = torch.stack([s.pack for s in squares])
         for s in squares:
-            s.row_sub_all.copy_(row_sub_all)
-            s.col_rec_all.copy_(col_rec_all)
-            s.status.copy_(status)
+            s.gathered.copy_(gathered)
             s.phase_finish()
         return squares

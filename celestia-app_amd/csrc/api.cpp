@@ -500,17 +500,15 @@ cel_status cel_dev_shard_cols(cel_ctx* ctx, void* d_slab, uint32_t k, uint32_t n
   return e == hipSuccess ? CEL_OK : hip_fail(ctx, e, "shard commit");
 }
 
-cel_status cel_dev_shard_finish(cel_ctx* ctx, const void* d_row_sub_all, const void* d_col_rec_all, uint32_t k,
-                                uint32_t nranks, void* d_row_roots, void* d_col_roots, void* d_dah,
-                                int32_t* d_status, void* d_work, void* stream, uint32_t flags) {
-  if (!ctx || !d_row_sub_all || !d_col_rec_all || !d_row_roots || !d_col_roots || !d_dah || !d_status || !d_work)
-    return CEL_EINVAL;
+cel_status cel_dev_shard_finish(cel_ctx* ctx, const void* d_gathered, uint32_t k, uint32_t nranks, void* d_row_roots,
+                                void* d_col_roots, void* d_dah, int32_t* d_status, void* d_work, void* stream,
+                                uint32_t flags) {
+  if (!ctx || !d_gathered || !d_row_roots || !d_col_roots || !d_dah || !d_status || !d_work) return CEL_EINVAL;
   std::lock_guard<std::mutex> lock(ctx->mu);
   cel_status st = validate_shard(ctx, k, nranks);
   if (st) return st;
   DeviceGuard g(ctx->device);
-  hipError_t e = launch_shard_finish(static_cast<const uint32_t*>(d_row_sub_all),
-                                     static_cast<const uint32_t*>(d_col_rec_all), k, nranks,
+  hipError_t e = launch_shard_finish(static_cast<const uint32_t*>(d_gathered), k, nranks,
                                      static_cast<uint8_t*>(d_row_roots), static_cast<uint8_t*>(d_col_roots),
                                      static_cast<uint8_t*>(d_dah), d_status, d_work,
                                      (flags & CEL_FLAG_ORDER_CHECK) != 0, pick_stream(ctx, stream));

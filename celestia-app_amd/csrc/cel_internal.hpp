@@ -116,9 +116,10 @@ size_t slab_workspace_size(uint32_t k, uint32_t w);
 hipError_t launch_slab_commit(const uint8_t* slab, uint32_t k, uint32_t c0, uint32_t w, uint32_t* col_rec,
                               uint32_t* row_sub, int32_t* status, void* work, bool order_check, hipStream_t s);
 size_t shard_finish_workspace_size(uint32_t k, uint32_t nranks);
-hipError_t launch_shard_finish(const uint32_t* row_subs, const uint32_t* col_rec, uint32_t k, uint32_t nranks,
-                               uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah, int32_t* status, void* work,
-                               bool order_check, hipStream_t s);
+// gathered: [nranks][2k + w + 1] records, rank order (row subtrees, column roots, status).
+hipError_t launch_shard_finish(const uint32_t* gathered, uint32_t k, uint32_t nranks, uint8_t* row_roots,
+                               uint8_t* col_roots, uint8_t* dah, int32_t* status, void* work, bool order_check,
+                               hipStream_t s);
 
 // Repair helpers (repair_kernels.hip, nmt_kernels.hip).
 hipError_t launch_gather_axes(const uint8_t* eds, const uint8_t* mask, uint32_t W, const int32_t* idx, int is_col,

@@ -621,15 +621,14 @@ __global__ CEL_LEVEL_BOUNDS void k_level_pair(LevelJob a, LevelJob b) {
 
 // Push order across slab boundaries (rows of Q0): the last leaf of slab r-1 must not
 // carry a larger namespace than the first leaf of slab r. Within a sorted slab those are
-// the subtree's maxNs and minNs. subs: [nranks][2k] records.
+// the subtree's maxNs and minNs. subs: rank r's 2k row-subtree records at subs[r * stride].
 __global__ void k_slab_boundary(const uint32_t* __restrict__ subs, uint32_t k, uint32_t w, uint32_t nranks,
-                                int32_t* __restrict__ bad_axis) {
+                                uint32_t stride, int32_t* __restrict__ bad_axis) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= k) return;
-  const uint32_t W = 2 * k;
   for (uint32_t r = 1; r < nranks && r * w < k; r++) {
-    const uint8_t* L = reinterpret_cast<const uint8_t*>(subs + ((uint64_t)(r - 1) * W + i) * kNodeWords);
-    const uint8_t* R = reinterpret_cast<const uint8_t*>(subs + ((uint64_t)r * W + i) * kNodeWords);
+    const uint8_t* L = reinterpret_cast<const uint8_t*>(subs + ((uint64_t)(r - 1) * stride + i) * kNodeWords);
+    const uint8_t* R = reinterpret_cast<const uint8_t*>(subs + ((uint64_t)r * stride + i) * kNodeWords);
     for (uint32_t b = 0; b < kNs; b++) {
       const uint8_t lm = L[kNs + b], rm = R[b];
       if (lm != rm) {
@@ -638,6 +637,19 @@ __global__ void k_slab_boundary(const uint32_t* __restrict__ subs, uint32_t k, u
       }
     }
   }
+}
+
+// status = max over the nranks gathered step-2 status records (first int32 of record
+// r * stride + at).
+__global__ void k_status_max(const uint32_t* __restrict__ gathered, uint32_t stride, uint32_t at, uint32_t nranks,
+                             int32_t* __restrict__ status) {
+  if (threadIdx.x != 0) return;
+  int32_t m = 0;
+  for (uint32_t r = 0; r < nranks; r++) {
+    const int32_t v = (int32_t)gathered[((uint64_t)r * stride + at) * kNodeWords];
+    m = v > m ? v : m;
+  }
+  *status = m;
 }
 
 __global__ void k_status_from_bad(const int32_t* __restrict__ bad_axis, int32_t* __restrict__ status) {
@@ -747,10 +759,12 @@ size_t shard_finish_workspace_size(uint32_t k, uint32_t nranks) {
   return 2 * align256(W * (nranks / 2 + 1) * nb) + align256(2 * W * nb) + 256 + align256(2 * W * 32);
 }
 
-hipError_t launch_shard_finish(const uint32_t* row_subs, const uint32_t* col_rec, uint32_t k, uint32_t nranks,
-                               uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah, int32_t* status, void* work,
-                               bool order_check, hipStream_t s) {
+hipError_t launch_shard_finish(const uint32_t* gathered, uint32_t k, uint32_t nranks, uint8_t* row_roots,
+                               uint8_t* col_roots, uint8_t* dah, int32_t* status, void* work, bool order_check,
+                               hipStream_t s) {
   const uint32_t W = 2 * k, w = W / nranks;
+  const uint32_t S = W + w + 1;  // records per rank: row subtrees, column roots, status
+  const uint32_t* row_subs = gathered;
   const size_t nb = kNodeWords * 4;
   uint8_t* base = static_cast<uint8_t*>(work);
   uint32_t* ping = reinterpret_cast<uint32_t*>(base);
@@ -764,12 +778,15 @@ hipError_t launch_shard_finish(const uint32_t* row_subs, const uint32_t* col_rec
   uint32_t* leafd = reinterpret_cast<uint32_t*>(base);
   hipLaunchKernelGGL(k_fill_i32, dim3(1), dim3(64), 0, s, bad, 1u, INT_MAX);
   if (order_check && nranks > 1)
-    hipLaunchKernelGGL(k_slab_boundary, dim3((k + 255) / 256), dim3(256), 0, s, row_subs, k, w, nranks, bad);
-  // row i's subtree from rank r is row_subs[r][i]: trees of nranks leaves, stride W
+    hipLaunchKernelGGL(k_slab_boundary, dim3((k + 255) / 256), dim3(256), 0, s, row_subs, k, w, nranks, S, bad);
+  // row i's subtree from rank r is gathered[r][i]: trees of nranks leaves, stride S
   if (nranks == 1) (void)hipMemcpyAsync(items, row_subs, (size_t)W * nb, hipMemcpyDeviceToDevice, s);
-  else reduce_grid(row_subs, nranks, W, 1, W, ping, pong, items, s);
-  (void)hipMemcpyAsync(items + (size_t)W * kNodeWords, col_rec, (size_t)W * nb, hipMemcpyDeviceToDevice, s);
-  // previous status (all-reduced over ranks by the caller) survives; boundary adds to it
+  else reduce_grid(row_subs, nranks, W, 1, S, ping, pong, items, s);
+  // the column roots: rank r's w records at gathered[r][W], in rank order
+  (void)hipMemcpy2DAsync(items + (size_t)W * kNodeWords, (size_t)w * nb, gathered + (size_t)W * kNodeWords,
+                         (size_t)S * nb, (size_t)w * nb, nranks, hipMemcpyDeviceToDevice, s);
+  // the ranks' step-2 status (max), then the push order across slab boundaries
+  hipLaunchKernelGGL(k_status_max, dim3(1), dim3(64), 0, s, gathered, S, W + w, nranks, status);
   hipLaunchKernelGGL(k_status_from_bad, dim3(1), dim3(64), 0, s, bad, status);
   // the 4k RFC-6962 leaf digests and the packed roots one lane each, then the DAH tree
   // one level per round in one workgroup

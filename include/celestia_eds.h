@@ -136,9 +136,9 @@ cel_status cel_dev_commit_only(cel_ctx* ctx, const void* d_eds, uint32_t n, uint
  * Replaces, for a square too large for one device's share of the work, the same
  * da.ExtendShares + NewDataAvailabilityHeader pair (data_availability_header.go:65-75,
  * :44-63). Rank r owns ODS rows [r*k/nranks, (r+1)*k/nranks) and, after the column
- * transpose, EDS columns [r*w, (r+1)*w) with w = 2k/nranks. The collectives (one
- * all-to-all, two all-gathers, one max-all-reduce of the status) belong to the caller
- * (RCCL through torch.distributed); these calls are the per-rank device steps.
+ * transpose, EDS columns [r*w, (r+1)*w) with w = 2k/nranks. The two collectives (one
+ * all-to-all of cells, one all-gather of node records) belong to the caller (RCCL
+ * through torch.distributed); these calls are the per-rank device steps.
  * Supported for k in {256, 512} (Leopard GF(2^16)), nranks a power of two <= k.
  * Node records are 96 bytes: the 90-byte NMT node and 6 zero bytes. */
 #define CEL_NODE_RECORD 96u
@@ -152,17 +152,20 @@ cel_status cel_dev_shard_rows(cel_ctx* ctx, const void* d_ods_rows, uint32_t k, 
  * with rows [0, k) received in rank order. Column-encodes the slab in place (rows
  * [k, 2k)), hashes its 2k*w leaves once, and writes the w column-root records
  * (d_col_rec: [w][96]) and the 2k row-subtree records over this slab's columns
- * (d_row_sub: [2k][96]). *d_status = 0 or CEL_EORDER (within-slab push order). */
+ * (d_row_sub: [2k][96]). *d_status = 0 or CEL_EORDER (within-slab push order).
+ * Step 3 all-gathers one record block per rank, [2k + w + 1][96]: the row subtrees,
+ * then the column roots, then a record whose first 4 bytes are the status; pointing
+ * d_row_sub, d_col_rec and d_status into that block makes it the send buffer. */
 cel_status cel_dev_shard_cols(cel_ctx* ctx, void* d_slab, uint32_t k, uint32_t nranks, uint32_t rank,
                               void* d_col_rec, void* d_row_sub, int32_t* d_status, void* d_work, void* stream,
                               uint32_t flags);
-/* Step 3 (after all-gathering the records of every rank, rank order):
- * d_row_sub_all [nranks][2k][96], d_col_rec_all [2k][96] -> d_row_roots, d_col_roots
- * (2k x 90 B each) and d_dah (32 B). *d_status (in: max over ranks of step 2) gains
- * CEL_EORDER if the push order breaks across slab boundaries. */
-cel_status cel_dev_shard_finish(cel_ctx* ctx, const void* d_row_sub_all, const void* d_col_rec_all, uint32_t k,
-                                uint32_t nranks, void* d_row_roots, void* d_col_roots, void* d_dah,
-                                int32_t* d_status, void* d_work, void* stream, uint32_t flags);
+/* Step 3 (after all-gathering every rank's record block, rank order):
+ * d_gathered [nranks][2k + w + 1][96] -> d_row_roots, d_col_roots (2k x 90 B each) and
+ * d_dah (32 B). *d_status = the max over ranks of the step-2 status, or CEL_EORDER if
+ * the push order breaks across slab boundaries. */
+cel_status cel_dev_shard_finish(cel_ctx* ctx, const void* d_gathered, uint32_t k, uint32_t nranks, void* d_row_roots,
+                                void* d_col_roots, void* d_dah, int32_t* d_status, void* d_work, void* stream,
+                                uint32_t flags);
 
 /* ------------------------------------------------------ rsmt2d.Codec surface
  * Leopard RS (klauspost/reedsolomon v1.12.1 New(n, n, WithLeopardGF(true))):

@@ -64,9 +64,12 @@ class OracleSteps:
             row_sub[i] = torch.from_numpy(record(root).copy())
         status[0] = EORDER if bad else 0
 
-    def finish(self, row_sub_all, col_rec_all, k, n, row_roots, col_roots, dah, status):
-        w = 2 * k // n
-        subs = row_sub_all.numpy()
+    def finish(self, gathered, k, n, row_roots, col_roots, dah, status):
+        w, W = 2 * k // n, 2 * k
+        g = gathered.numpy()
+        subs = g[:, :W]
+        col_rec_all = torch.from_numpy(np.ascontiguousarray(g[:, W:W + w]).reshape(W, -1))
+        st = int(max(np.frombuffer(g[r, W + w, :4].tobytes(), np.int32)[0] for r in range(n)))
         bad = False
         for i in range(2 * k):
             nodes = [subs[r, i, :90].tobytes() for r in range(n)]
@@ -79,5 +82,4 @@ class OracleSteps:
             row_roots[i] = torch.from_numpy(np.frombuffer(nodes[0], np.uint8).copy())
         col_roots.copy_(col_rec_all[:, :90])
         dah.copy_(torch.from_numpy(np.frombuffer(oracle.dah_hash(row_roots.numpy(), col_roots.numpy()), np.uint8).copy()))
-        if bad:
-            status[0] = EORDER
+        status[0] = EORDER if bad else st

@@ -97,9 +97,6 @@ def test_one_rank_aliases_slab(oracle, local):
             def all_gather(self, out, inp):
                 out.copy_(inp)
 
-            def all_reduce_max(self, t):
-                pass
-
             def all_to_all(self, out, inp):
                 raise AssertionError("one rank must not exchange")
         sq.run(NoComm())

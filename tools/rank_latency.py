@@ -31,8 +31,7 @@ sq = ShardedSquare(a.k, 0, a.n, steps)
 lo, hi = sq.row_range()
 sq.ods_rows.copy_(torch.from_numpy(np.ascontiguousarray(random_ods(a.k, 512)[lo:hi])))
 sq.slab.copy_(torch.from_numpy(np.ascontiguousarray(random_ods(2 * a.k, 5)[:, : sq.w])))  # stand-in slab
-sq.row_sub_all.zero_()
-sq.col_rec_all.zero_()
+sq.gathered.zero_()
 cur = steps.stream
 
 
