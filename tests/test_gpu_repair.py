@@ -248,21 +248,26 @@ def test_k128_one_corrupt_cell(ctx, oracle, p):
     assert all(s == bs[j].tobytes() for j, s in enumerate(e.Shares) if s is not None)
 
 
-def test_sanity_check_bad_encoding(ctx, oracle):
-    """Every cell present, row 3's parity half changed, and roots computed over that
-    square: every root matches, so only rsmt2d's re-encoding of complete axes in
-    preRepairSanityCheck catches it (ErrByzantineData, row 3, all its shares)."""
+@pytest.mark.parametrize("k", [16, 32, 64, 128])
+@pytest.mark.parametrize("in_q1", [True, False])
+def test_sanity_check_bad_encoding(ctx, oracle, k, in_q1):
+    """Every cell present, one parity cell changed, and roots computed over that square:
+    every root matches, so only rsmt2d's re-encoding of complete axes in
+    preRepairSanityCheck catches it (ErrByzantineData with all the axis's shares). Cell
+    (3, k+1) breaks row 3 and column k+1, reported as row 3; cell (k+1, 3) breaks row k+1
+    and column 3, reported as column 3 (rsmt2d checks row i, then column i). k >= 32:
+    the in-place check kernel in both directions; k = 16: gather -> encode -> compare."""
     from celestia_eds import _lib
-    k = 16
     w = 2 * k
     eds, _, _ = setup(oracle, k, seed=3)
-    eds[3, k + 1, 100] ^= 0x77  # Q1 cell: row 3 and column k + 1 are no longer codewords
+    r, c = (3, k + 1) if in_q1 else (k + 1, 3)
+    eds[r, c, 100] ^= 0x77
     _, rr, cr = oracle.roots(eds, check_order=False)
     present = np.ones((w, w), np.uint8)
     st, bad, bs, bp = _assert_same_outcome(ctx, oracle, eds, present, [x.tobytes() for x in rr],
                                            [x.tobytes() for x in cr])
-    assert st == _lib.EBYZANTINE and bad == (0, 3)
-    assert bp.all() and np.array_equal(bs, eds[3])
+    assert st == _lib.EBYZANTINE and bad == ((0, 3) if in_q1 else (1, 3))
+    assert bp.all() and np.array_equal(bs, eds[3] if in_q1 else eds[:, 3])
 
 
 def test_sanity_check_bad_root(ctx, oracle):
