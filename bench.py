@@ -89,6 +89,9 @@ def parse():
     ap.add_argument("--no-riders", action="store_true",
                     help="with --k 128: skip the config-4 (k64) and config-3 (rowshard512) riders")
     ap.add_argument("--rider-steps", type=int, default=5)
+    ap.add_argument("--depth", type=int, default=2,
+                    help="row-sharded square (--mode sharded and the rowshard512 rider): squares in flight "
+                         "per step of the pipelined measurement (the plain value keeps one in flight)")
     ap.add_argument("--rehearse", action="store_true",
                     help="multi-rank rehearsal on a one-GPU box: every rank on cuda:0, gloo instead of RCCL "
                          "(collectives staged through host memory); exercises the N-rank code path, its "
@@ -209,19 +212,14 @@ def run_sharded(a):
     local = _rank_device(local)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    from celestia_eds import default_context
-    from celestia_eds.sharded import DeviceSteps, LocalComm, ShardedSquare
-    from celestia_eds.testfactory import random_ods
+    from celestia_eds.sharded import LocalComm, run_pipelined
     dist = None
     if world > 1:
         dist = _init_dist(dev)
     k = a.k
-    ctx = default_context(local)
-    steps = DeviceSteps(ctx, local)
-    sq = ShardedSquare(k, rank, world, steps)
-    ods = random_ods(k, 512)
-    lo, hi = sq.row_range()
-    sq.ods_rows.copy_(torch.from_numpy(np.ascontiguousarray(ods[lo:hi])))
+    sqs = _sharded_squares(k, world, rank, local, max(1, a.depth))
+    sq = sqs[0]
+    steps = sq.steps
     comm = _comm() if dist is not None else None
 
     def step():
@@ -247,6 +245,13 @@ def run_sharded(a):
     torch.cuda.synchronize()
     elapsed = _max_over_ranks(time.perf_counter() - t0, dist, dev)
     sq.check_status()
+    piped = None
+    if a.depth > 1:
+        e_p = _timed_steps(lambda: run_pipelined(sqs, comm), a.steps, a.warmup, barrier, dist, dev)
+        for s in sqs:
+            s.check_status()
+        piped = {"squares_in_flight": a.depth, "value": a.depth * a.steps / e_p, "unit": "squares/s",
+                 "ms_per_square": e_p / (a.depth * a.steps) * 1e3}
     # rank-local phase timing (HIP events on the launch stream of the device steps)
     cur = steps.stream
 
@@ -300,6 +305,7 @@ def run_sharded(a):
             "avg_launch_us": t_rows * 1e6,
         },
         "phase_us": {"rows": t_rows * 1e6, "cols_and_commit": t_cols * 1e6},
+        "pipelined": piped,
     }
     if rank == 0:
         print(json.dumps(result), flush=True)
@@ -609,25 +615,7 @@ def _max_over_ranks(x, dist, dev):
     return float(t.item())
 
 
-def measure_rowshard(k, world, rank, local, dist, dev, steps, warmup, barrier):
-    """The run_sharded schedule as a rider of the batch line: full steps (barrier-bracketed,
-    max over ranks), then the all-to-all alone (median of 5, max over ranks)."""
-    from celestia_eds import default_context
-    from celestia_eds.sharded import DeviceSteps, LocalComm, ShardedSquare
-    from celestia_eds.testfactory import random_ods
-    ctx = default_context(local)
-    dsteps = DeviceSteps(ctx, local)
-    sq = ShardedSquare(k, rank, world, dsteps)
-    lo, hi = sq.row_range()
-    sq.ods_rows.copy_(torch.from_numpy(np.ascontiguousarray(random_ods(k, 512)[lo:hi])))
-    comm = _comm() if dist is not None else None
-
-    def step():
-        if comm is not None:
-            sq.run(comm)
-        else:
-            LocalComm.run([sq])
-
+def _timed_steps(step, steps, warmup, barrier, dist, dev):
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
@@ -639,8 +627,49 @@ def measure_rowshard(k, world, rank, local, dist, dev, steps, warmup, barrier):
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
-    elapsed = _max_over_ranks(time.perf_counter() - t0, dist, dev)
+    return _max_over_ranks(time.perf_counter() - t0, dist, dev)
+
+
+def _sharded_squares(k, world, rank, local, depth):
+    """`depth` independent row-sharded squares of this rank, each with its own device
+    steps (stream and workspace), loaded with distinct synthetic ODS rows."""
+    from celestia_eds import default_context
+    from celestia_eds.sharded import DeviceSteps, ShardedSquare
+    from celestia_eds.testfactory import random_ods
+    ctx = default_context(local)
+    sqs = []
+    for d in range(depth):
+        sq = ShardedSquare(k, rank, world, DeviceSteps(ctx, local))
+        lo, hi = sq.row_range()
+        sq.ods_rows.copy_(torch.from_numpy(np.ascontiguousarray(random_ods(k, 512 + d)[lo:hi])))
+        sqs.append(sq)
+    return sqs
+
+
+def measure_rowshard(k, world, rank, local, dist, dev, steps, warmup, barrier, depth=2):
+    """The run_sharded schedule as a rider of the batch line: full steps (barrier-bracketed,
+    max over ranks) with one square in flight, the same with `depth` squares in flight
+    (sharded.run_pipelined), then the all-to-all alone (median of 5, max over ranks)."""
+    from celestia_eds.sharded import LocalComm, run_pipelined
+    comm = _comm() if dist is not None else None
+    sqs = _sharded_squares(k, world, rank, local, max(1, depth))
+    sq = sqs[0]
+
+    def step():
+        if comm is not None:
+            sq.run(comm)
+        else:
+            LocalComm.run([sq])
+
+    elapsed = _timed_steps(step, steps, warmup, barrier, dist, dev)
     sq.check_status()
+    piped = None
+    if depth > 1:
+        e_p = _timed_steps(lambda: run_pipelined(sqs, comm), steps, warmup, barrier, dist, dev)
+        for s in sqs:
+            s.check_status()
+        piped = {"squares_in_flight": depth, "value": depth * steps / e_p, "unit": "squares/s",
+                 "ms_per_square": e_p / (depth * steps) * 1e3}
     t_a2a = 0.0
     if comm is not None:
         ts = []
@@ -653,8 +682,12 @@ def measure_rowshard(k, world, rank, local, dist, dev, steps, warmup, barrier):
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t1)
         t_a2a = _max_over_ranks(sorted(ts)[2], dist, dev)
-    del sq
-    return _rowshard_fields(k, world, elapsed, steps, t_a2a)
+    del sq, sqs
+    f = _rowshard_fields(k, world, elapsed, steps, t_a2a)
+    f["latency_ms"] = elapsed / steps * 1e3
+    if piped:
+        f["pipelined"] = piped
+    return f
 
 
 def _measure_batch(ctx, local, rank, k, B, steps, warmup, n_distinct, layout, phase_reps, barrier, dist, dev):
@@ -899,7 +932,8 @@ def main():
         result["k64"] = _k64_fields(world, m4["elapsed"], a.rider_steps, m4["t_ext"], m4["t_com"], 1024 // world)
         del m4
         torch.cuda.empty_cache()
-        result["rowshard512"] = measure_rowshard(512, world, rank, local, dist, dev, a.rider_steps, 2, barrier)
+        result["rowshard512"] = measure_rowshard(512, world, rank, local, dist, dev, a.rider_steps, 2, barrier,
+                                                 a.depth)
         torch.cuda.empty_cache()
     if rank == 0 and world == 1 and a.k == 128 and not a.no_host_io:
         result["host_io"] = measure_host_io(ctx, a.k)

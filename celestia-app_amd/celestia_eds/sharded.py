@@ -188,6 +188,30 @@ class ShardedSquare:
             raise _lib.CelError(st, "invalid push order: leaf namespaces must be non-decreasing")
 
 
+def run_pipelined(squares, comm):
+    """Several independent squares in flight on one rank (each ShardedSquare with its own
+    DeviceSteps: own stream and workspace), phases interleaved so one square's
+    latency-bound tree levels overlap another's encode and leaf hashing. Every rank issues
+    the collectives in the same order (square 0's all-to-all, square 1's, ..., then the
+    gathers), as RCCL requires. comm None: one rank, no collectives."""
+    for sq in squares:
+        with sq.scope():
+            sq.phase_rows()
+            if comm is not None:
+                sq.exchange(comm)
+    for sq in squares:
+        with sq.scope():
+            sq.phase_cols()
+            if comm is not None:
+                sq.gather(comm)
+            else:
+                sq.gathered[0].copy_(sq.pack)
+    for sq in squares:
+        with sq.scope():
+            sq.phase_finish()
+    return squares
+
+
 class LocalComm:
     """Collectives among ShardedSquare objects of one process (single-GPU rehearsal of
     the N-rank schedule: same buffers, same layouts, copies instead of RCCL)."""

@@ -127,3 +127,73 @@ def test_device_sharded_local(ctx, oracle, k, n):
         assert np.array_equal(s.row_roots.cpu().numpy(), rr)
         assert np.array_equal(s.col_roots.cpu().numpy(), cr)
         assert s.dah.cpu().numpy().tobytes() == dah
+
+
+def _worker_pipelined(rank, world, port, k, seeds, out_q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "celestia-app_amd"), os.path.join(root, "oracle"), os.path.join(root, "tests")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    from celestia_eds.sharded import ShardedSquare, TorchComm, run_pipelined
+    from sharded_oracle import OracleSteps
+    from eds_inputs import random_ods as rods
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sqs = []
+        for sd in seeds:
+            sq = ShardedSquare(k, rank, world, OracleSteps())
+            a, b = sq.row_range()
+            sq.ods_rows.copy_(torch.from_numpy(np.ascontiguousarray(rods(k, sd)[a:b])))
+            sqs.append(sq)
+        run_pipelined(sqs, TorchComm())
+        out_q.put((rank, [(s.row_roots.numpy().copy(), s.col_roots.numpy().copy(), s.dah.numpy().tobytes(),
+                           int(s.status.item())) for s in sqs]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_pipelined_squares(oracle):
+    """Several squares in flight per rank (sharded.run_pipelined: every rank issues the
+    all-to-alls of all squares, then their gathers, in the same order), world 2 over gloo:
+    each square's roots and DAH are its own whole-square result."""
+    world, k, seeds = 2, 8, (41, 42, 43)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_pipelined, args=(r, world, port, k, seeds, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for sd, i in zip(seeds, range(len(seeds))):
+        _, rr, cr, dah = oracle.extend_and_commit(random_ods(k, sd), want_eds=False)
+        for rank, outs in res:
+            r_rr, r_cr, r_dah, st = outs[i]
+            assert st == 0 and np.array_equal(r_rr, rr) and np.array_equal(r_cr, cr) and r_dah == dah, (rank, sd)
+
+
+@pytest.mark.gpu
+def test_device_pipelined_one_rank(ctx, oracle):
+    """Three k=256 squares in flight on one GPU (each with its own stream and workspace,
+    sharded.run_pipelined without collectives): each equals the oracle's whole square."""
+    from celestia_eds.sharded import DeviceSteps, ShardedSquare, run_pipelined
+    k, seeds = 256, (61, 62, 63)
+    sqs = []
+    for sd in seeds:
+        sq = ShardedSquare(k, 0, 1, DeviceSteps(ctx))
+        sq.ods_rows.copy_(torch.from_numpy(random_ods(k, sd)))
+        sqs.append(sq)
+    for _ in range(2):  # twice: the second round reuses every buffer
+        run_pipelined(sqs, None)
+    torch.cuda.synchronize()
+    for sd, sq in zip(seeds, sqs):
+        eds, rr, cr, dah = oracle.extend_and_commit(random_ods(k, sd))
+        assert int(sq.status.item()) == 0
+        assert np.array_equal(sq.slab.cpu().numpy(), eds)
+        assert np.array_equal(sq.row_roots.cpu().numpy(), rr) and np.array_equal(sq.col_roots.cpu().numpy(), cr)
+        assert sq.dah.cpu().numpy().tobytes() == dah
