@@ -89,7 +89,7 @@ def parse():
     ap.add_argument("--no-riders", action="store_true",
                     help="with --k 128: skip the config-4 (k64) and config-3 (rowshard512) riders")
     ap.add_argument("--rider-steps", type=int, default=5)
-    ap.add_argument("--depth", type=int, default=2,
+    ap.add_argument("--depth", type=int, default=4,
                     help="row-sharded square (--mode sharded and the rowshard512 rider): squares in flight "
                          "per step of the pipelined measurement (the plain value keeps one in flight)")
     ap.add_argument("--rehearse", action="store_true",

@@ -86,15 +86,33 @@ constexpr uint32_t kLeafParPrefix[7] = {0x00FFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0
                                         0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
 constexpr ShaMid kLeafParMid = sha_midstate(kLeafParPrefix, 7);
 
+// PF (prefetch): the next block's words are loaded while the current block is compressed.
+// At one or two waves per SIMD (a single square's commit, a rank's slab) nothing else
+// covers a block's load latency, which the plain form exposes nine times per leaf; at
+// batch occupancy other waves cover it and the 17 extra VGPRs cost 1.5-3 %
+// (profiles/r2_nmt_leaf_prefetch_ab.txt), so the batch keeps PF = false.
+template <bool PF>
 __device__ __forceinline__ void leaf_hash(uint32_t (&st)[8], const uint32_t* __restrict__ sh, bool q0) {
   sha256_init(st);
   uint32_t w[16];
+  uint32_t nx[17];  // PF: the next block's share dwords
+  auto load17 = [&](int b) {  // share bytes [64b-30, 64b+34) for block b = 1..7
+    const uint32_t* base = sh + 16 * b - 8;
+    const uint4* p4 = reinterpret_cast<const uint4*>(base);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const uint4 v = p4[i];
+      nx[4 * i] = v.x; nx[4 * i + 1] = v.y; nx[4 * i + 2] = v.z; nx[4 * i + 3] = v.w;
+    }
+    nx[16] = base[16];
+  };
   {  // block 0: 0x00 || ns || share[0:34]
     uint32_t s[9];
     const uint4* p4 = reinterpret_cast<const uint4*>(sh);
     const uint4 v0 = p4[0], v1 = p4[1];
     s[0] = v0.x; s[1] = v0.y; s[2] = v0.z; s[3] = v0.w; s[4] = v1.x; s[5] = v1.y; s[6] = v1.z; s[7] = v1.w;
     s[8] = sh[8];
+    if (PF) load17(1);
 #pragma unroll
     for (int i = 8; i < 16; i++) w[i] = perm(s[i - 8], s[i - 7], 0x06070001u);
     if (__all(!q0)) {  // wave-uniform parity cells: rounds 0..6 are one constant
@@ -118,27 +136,29 @@ __device__ __forceinline__ void leaf_hash(uint32_t (&st)[8], const uint32_t* __r
   }
 #pragma unroll 1
   for (int b = 1; b < 8; b++) {  // blocks 1..7: share bytes [64b-30, 64b+34)
-    const uint32_t* base = sh + 16 * b - 8;
-    const uint4* p4 = reinterpret_cast<const uint4*>(base);
-    uint32_t s[17];
+    if (!PF) load17(b);
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const uint4 v = p4[i];
-      s[4 * i] = v.x; s[4 * i + 1] = v.y; s[4 * i + 2] = v.z; s[4 * i + 3] = v.w;
+    for (int i = 0; i < 16; i++) w[i] = perm(nx[i], nx[i + 1], 0x06070001u);
+    if (PF) {
+      if (b < 7) {
+        load17(b + 1);
+      } else {  // the last block's 8 dwords
+        const uint4* p4 = reinterpret_cast<const uint4*>(sh + 120);
+        const uint4 v0 = p4[0], v1 = p4[1];
+        nx[0] = v0.x; nx[1] = v0.y; nx[2] = v0.z; nx[3] = v0.w; nx[4] = v1.x; nx[5] = v1.y; nx[6] = v1.z; nx[7] = v1.w;
+      }
     }
-    s[16] = base[16];
-#pragma unroll
-    for (int i = 0; i < 16; i++) w[i] = perm(s[i], s[i + 1], 0x06070001u);
     sha256_compress(st, w);
   }
   {  // block 8: share[482:512] || 0x80 || 0... || len
-    const uint4* p4 = reinterpret_cast<const uint4*>(sh + 120);
-    uint32_t s[8];
-    const uint4 v0 = p4[0], v1 = p4[1];
-    s[0] = v0.x; s[1] = v0.y; s[2] = v0.z; s[3] = v0.w; s[4] = v1.x; s[5] = v1.y; s[6] = v1.z; s[7] = v1.w;
+    if (!PF) {
+      const uint4* p4 = reinterpret_cast<const uint4*>(sh + 120);
+      const uint4 v0 = p4[0], v1 = p4[1];
+      nx[0] = v0.x; nx[1] = v0.y; nx[2] = v0.z; nx[3] = v0.w; nx[4] = v1.x; nx[5] = v1.y; nx[6] = v1.z; nx[7] = v1.w;
+    }
 #pragma unroll
-    for (int i = 0; i < 7; i++) w[i] = perm(s[i], s[i + 1], 0x06070001u);
-    w[7] = perm(s[7], 0x80u, 0x0607000Cu);
+    for (int i = 0; i < 7; i++) w[i] = perm(nx[i], nx[i + 1], 0x06070001u);
+    w[7] = perm(nx[7], 0x80u, 0x0607000Cu);
 #pragma unroll
     for (int i = 8; i < 15; i++) w[i] = 0u;
     w[15] = 542u * 8u;
@@ -169,9 +189,10 @@ __device__ __forceinline__ bool ns_less(const uint32_t* __restrict__ a, const ui
 
 // Leaf node of one EDS cell: ns || ns || SHA256(0x00 || ns || share), ns = share[0:29]
 // for Q0 cells and 0xFF*29 (parity namespace) otherwise.
+template <bool PF>
 __device__ __forceinline__ void make_leaf_node(const uint32_t* __restrict__ sh, bool q0, uint32_t (&nd)[kNodeWords]) {
   uint32_t st[8];
-  leaf_hash(st, sh, q0);
+  leaf_hash<PF>(st, sh, q0);
   if (q0) {
     const uint4* p4 = reinterpret_cast<const uint4*>(sh);
     uint32_t s[8];
@@ -192,7 +213,7 @@ __device__ __forceinline__ void make_leaf_node(const uint32_t* __restrict__ sh, 
 }
 
 // grid: x = cell block (256 cells), y = square. Writes leaf nodes [sq][W*W][24].
-template <bool ORDER>
+template <bool ORDER, bool PF>
 __global__ CEL_LEAF_BOUNDS void k_leaf(const uint8_t* __restrict__ eds, uint32_t k, uint32_t* __restrict__ leaves,
                                               int32_t* __restrict__ bad_axis) {
   const uint32_t W = 2 * k;
@@ -204,7 +225,7 @@ __global__ CEL_LEAF_BOUNDS void k_leaf(const uint8_t* __restrict__ eds, uint32_t
   const bool q0 = (r < k) && (c < k);
   {
     uint32_t nd[kNodeWords];
-    make_leaf_node(sh, q0, nd);
+    make_leaf_node<PF>(sh, q0, nd);
     store_node(leaves + ((uint64_t)blockIdx.y * W * W + cell) * kNodeWords, nd);
   }
   // The push-order check runs after the hash: done first, its share prefixes stay live
@@ -484,6 +505,10 @@ __global__ void k_fill_i32(int32_t* p, uint32_t n, int32_t v) {
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// A leaf launch of this many lanes leaves at most two waves per SIMD (1024 SIMDs): load
+// latency is then exposed and the prefetching leaf hash (leaf_hash<true>) pays.
+static bool latency_bound(uint64_t lanes) { return lanes <= 2ull * 1024 * 64; }
+
 // Workspace: leaves [nsq][W*W] nodes | ping [nsq][2W][W/2] | pong [nsq][2W][W/4] |
 //            roots [nsq][2W] nodes | bad_axis [nsq] int32 | DAH leaf digests [nsq][2W][8]
 size_t nmt_workspace_size(uint32_t k, uint32_t nsq) {
@@ -514,8 +539,13 @@ hipError_t launch_commit(const uint8_t* eds, uint32_t k, uint32_t nsq, uint8_t* 
     const Range r("nmt.leaf");
     hipLaunchKernelGGL(k_fill_i32, dim3((nsq + 255) / 256), dim3(256), 0, s, bad, nsq, INT_MAX);
     dim3 gl((W * W + 255) / 256, nsq);
-    if (order_check) hipLaunchKernelGGL(k_leaf<true>, gl, dim3(256), 0, s, eds, k, leaves, bad);
-    else hipLaunchKernelGGL(k_leaf<false>, gl, dim3(256), 0, s, eds, k, leaves, bad);
+    if (latency_bound(W * W * nsq)) {
+      if (order_check) hipLaunchKernelGGL((k_leaf<true, true>), gl, dim3(256), 0, s, eds, k, leaves, bad);
+      else hipLaunchKernelGGL((k_leaf<false, true>), gl, dim3(256), 0, s, eds, k, leaves, bad);
+    } else {
+      if (order_check) hipLaunchKernelGGL((k_leaf<true, false>), gl, dim3(256), 0, s, eds, k, leaves, bad);
+      else hipLaunchKernelGGL((k_leaf<false, false>), gl, dim3(256), 0, s, eds, k, leaves, bad);
+    }
   }
 
   // One launch per tree level, all 4k trees of all squares at once: every lane hashes
@@ -559,7 +589,7 @@ hipError_t launch_commit(const uint8_t* eds, uint32_t k, uint32_t nsq, uint8_t* 
 // range, hence a subtree of the row's perfect tree). Rank-ordered subtree roots are
 // combined into the row roots after an all-gather.
 
-template <bool ORDER>
+template <bool ORDER, bool PF>
 __global__ CEL_LEAF_BOUNDS void k_slab_leaf(const uint8_t* __restrict__ slab, uint32_t k, uint32_t c0, uint32_t w,
                                             uint32_t* __restrict__ leaves, int32_t* __restrict__ bad_axis) {
   const uint32_t W = 2 * k;
@@ -573,7 +603,7 @@ __global__ CEL_LEAF_BOUNDS void k_slab_leaf(const uint8_t* __restrict__ slab, ui
     if (i > 0 && ns_less(sh, sh - (uint64_t)w * kShare / 4)) atomicMin(bad_axis, (int32_t)(W + c));
   }
   uint32_t nd[kNodeWords];
-  make_leaf_node(sh, q0, nd);
+  make_leaf_node<PF>(sh, q0, nd);
   store_node(leaves + (uint64_t)cell * kNodeWords, nd);
 }
 
@@ -741,8 +771,13 @@ hipError_t launch_slab_commit(const uint8_t* slab, uint32_t k, uint32_t c0, uint
   hipLaunchKernelGGL(k_fill_i32, dim3(1), dim3(64), 0, s, bad, 1u, INT_MAX);
   hipLaunchKernelGGL(k_fill_i32, dim3(1), dim3(64), 0, s, status, 1u, 0);
   dim3 gl((W * w + 255) / 256);
-  if (order_check) hipLaunchKernelGGL(k_slab_leaf<true>, gl, dim3(256), 0, s, slab, k, c0, w, leaves, bad);
-  else hipLaunchKernelGGL(k_slab_leaf<false>, gl, dim3(256), 0, s, slab, k, c0, w, leaves, bad);
+  if (latency_bound(W * w)) {
+    if (order_check) hipLaunchKernelGGL((k_slab_leaf<true, true>), gl, dim3(256), 0, s, slab, k, c0, w, leaves, bad);
+    else hipLaunchKernelGGL((k_slab_leaf<false, true>), gl, dim3(256), 0, s, slab, k, c0, w, leaves, bad);
+  } else {
+    if (order_check) hipLaunchKernelGGL((k_slab_leaf<true, false>), gl, dim3(256), 0, s, slab, k, c0, w, leaves, bad);
+    else hipLaunchKernelGGL((k_slab_leaf<false, false>), gl, dim3(256), 0, s, slab, k, c0, w, leaves, bad);
+  }
   // w column trees of 2k leaves (leaf i of column j at i*w + j) and 2k row subtrees of w
   // leaves (leaf j of row i at i*w + j), both sets one level per launch
   if (w == 1) (void)hipMemcpyAsync(row_sub, leaves, (size_t)W * nb, hipMemcpyDeviceToDevice, s);
@@ -854,7 +889,7 @@ __global__ __launch_bounds__(256) void k_axis_leaf(const uint8_t* __restrict__ c
   const uint32_t* sh = reinterpret_cast<const uint32_t*>(cells + (uint64_t)i * kShare);
   const bool q0 = (i < k) && (axis < k);
   uint32_t st[8];
-  leaf_hash(st, sh, q0);
+  leaf_hash<true>(st, sh, q0);
   uint32_t nd[kNodeWords];
   if (q0) {
     uint32_t s[8];
@@ -951,7 +986,7 @@ __global__ __launch_bounds__(256) void k_axes_leaf(const uint8_t* __restrict__ c
   const uint32_t* sh = reinterpret_cast<const uint32_t*>(cells + (uint64_t)g * kShare);
   const bool q0 = (i < k) && ((uint32_t)axis_idx[a] < k);
   uint32_t st[8];
-  leaf_hash(st, sh, q0);
+  leaf_hash<true>(st, sh, q0);
   uint32_t nd[kNodeWords];
   if (q0) {
     uint32_t s[8];
