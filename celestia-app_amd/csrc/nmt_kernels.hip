@@ -780,7 +780,10 @@ hipError_t launch_slab_commit(const uint8_t* slab, uint32_t k, uint32_t c0, uint
   }
   // w column trees of 2k leaves (leaf i of column j at i*w + j) and 2k row subtrees of w
   // leaves (leaf j of row i at i*w + j), both sets one level per launch
-  if (w == 1) (void)hipMemcpyAsync(row_sub, leaves, (size_t)W * nb, hipMemcpyDeviceToDevice, s);
+  if (w == 1) {
+    const hipError_t e = hipMemcpyAsync(row_sub, leaves, (size_t)W * nb, hipMemcpyDeviceToDevice, s);
+    if (e != hipSuccess) return e;
+  }
   const LevelJob cols{leaves, nullptr, W, w, 1, w};
   const LevelJob rows{leaves, nullptr, w, W, w, 1};
   reduce_grid_pair(cols, ping, pong, col_rec, rows, ping2, pong2, row_sub, s);
@@ -815,11 +818,14 @@ hipError_t launch_shard_finish(const uint32_t* gathered, uint32_t k, uint32_t nr
   if (order_check && nranks > 1)
     hipLaunchKernelGGL(k_slab_boundary, dim3((k + 255) / 256), dim3(256), 0, s, row_subs, k, w, nranks, S, bad);
   // row i's subtree from rank r is gathered[r][i]: trees of nranks leaves, stride S
-  if (nranks == 1) (void)hipMemcpyAsync(items, row_subs, (size_t)W * nb, hipMemcpyDeviceToDevice, s);
+  hipError_t e = hipSuccess;
+  if (nranks == 1) e = hipMemcpyAsync(items, row_subs, (size_t)W * nb, hipMemcpyDeviceToDevice, s);
   else reduce_grid(row_subs, nranks, W, 1, S, ping, pong, items, s);
   // the column roots: rank r's w records at gathered[r][W], in rank order
-  (void)hipMemcpy2DAsync(items + (size_t)W * kNodeWords, (size_t)w * nb, gathered + (size_t)W * kNodeWords,
+  if (e == hipSuccess)
+    e = hipMemcpy2DAsync(items + (size_t)W * kNodeWords, (size_t)w * nb, gathered + (size_t)W * kNodeWords,
                          (size_t)S * nb, (size_t)w * nb, nranks, hipMemcpyDeviceToDevice, s);
+  if (e != hipSuccess) return e;
   // the ranks' step-2 status (max), then the push order across slab boundaries
   hipLaunchKernelGGL(k_status_max, dim3(1), dim3(64), 0, s, gathered, S, W + w, nranks, status);
   hipLaunchKernelGGL(k_status_from_bad, dim3(1), dim3(64), 0, s, bad, status);
