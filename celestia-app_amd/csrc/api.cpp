@@ -856,6 +856,7 @@ struct RepairBufs {
   uint32_t W;
   uint8_t* eds;
   uint8_t* mask;
+  int32_t* list0;     // the first pass's axis list, right after the mask (one upload for both)
   uint8_t* dense[2];  // gathered axes of the solve passes, alternating (main stream)
   uint8_t* dmask;
   uint8_t* dchk;      // gathered axes of the check passes (side stream)
@@ -966,14 +967,16 @@ struct Issued {
 };
 
 static cel_status solve_issue(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_col, const std::vector<int32_t>& list,
-                              Issued* out) {
+                              Issued* out, int32_t* uploaded = nullptr) {
   const Range range("repair.solve");
   const uint32_t W = 2 * k, na = (uint32_t)list.size();
   out->na = na;
   if (!na) return CEL_OK;
   const uint32_t d = out->d = b.solves++ & 1u;
   cel_status st;
-  if ((st = upload_list(ctx, b, list, b.main, &out->idx)) != CEL_OK || (st = fuzz(ctx, b.main)) != CEL_OK) return st;
+  if (uploaded) out->idx = uploaded;  // `list` is already on the device there
+  else if ((st = upload_list(ctx, b, list, b.main, &out->idx)) != CEL_OK) return st;
+  if ((st = fuzz(ctx, b.main)) != CEL_OK) return st;
   const int32_t* idx = out->idx;
   hipError_t e;
   if (rs_decode_axis_supported(W, kShare)) {
@@ -1490,13 +1493,9 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
     hipStream_t side;
     ~SideDrain() { (void)hipStreamSynchronize(side); }
   } drain{b.side};
-  std::memcpy(b.hmask, hm.data(), cells);
-  if ((e = hipMemcpyAsync(b.mask, b.hmask, cells, hipMemcpyHostToDevice, s)) != hipSuccess ||
-      (e = hipMemsetAsync(b.flags, 0, 2 * (size_t)W * 4, s)) != hipSuccess ||
-      (e = hipEventRecord(b.ev_main, s)) != hipSuccess || (e = hipStreamWaitEvent(b.side, b.ev_main, 0)) != hipSuccess)
-    return hip_fail(ctx, e, "H2D");
   // The first row pass goes to the device before the host builds its bookkeeping (the
-  // mask bitsets, the sanity lists), which then runs beside the decode.
+  // mask bitsets, the sanity lists), which then runs beside the decode; its axis list
+  // rides in the mask's upload.
   std::vector<int32_t> list, orth, first;
   for (uint32_t i = 0; i < W; i++) {  // hm bytes are 0 / 1: a word's popcount is its count
     const uint8_t* r = hm.data() + (size_t)i * W;
@@ -1510,13 +1509,21 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
     for (; j < W; j++) c += r[j];
     if (c >= k && c < W) first.push_back((int32_t)i);
   }
+  const size_t cells_a = (cells + 255) & ~(size_t)255;
+  std::memcpy(b.hmask, hm.data(), cells);
+  if (!first.empty()) std::memcpy(b.hmask + cells_a, first.data(), first.size() * 4);
+  // the flags are the side stream's (its checks), zeroed there after the mask is up
+  if ((e = hipMemcpyAsync(b.mask, b.hmask, cells_a + first.size() * 4, hipMemcpyHostToDevice, s)) != hipSuccess ||
+      (e = hipEventRecord(b.ev_main, s)) != hipSuccess || (e = hipStreamWaitEvent(b.side, b.ev_main, 0)) != hipSuccess ||
+      (e = hipMemsetAsync(b.flags, 0, 2 * (size_t)W * 4, b.side)) != hipSuccess)
+    return hip_fail(ctx, e, "H2D");
   // Each pass's encoding check (side stream) is enqueued after the next pass's decode, so
   // the host's enqueue of it is off the solve chain (the checked axes are final from their
   // pass on; the dense path's buffer dense[d] is reused two passes later, after the check
   // has recorded ev_side[d]).
   Issued prev;
   int prev_col = 0;
-  if ((st = solve_issue(ctx, b, k, 0, first, &prev)) != CEL_OK) return st;
+  if ((st = solve_issue(ctx, b, k, 0, first, &prev, b.list0)) != CEL_OK) return st;
   bool first_issued = !first.empty();
   std::unique_ptr<Range> plan_range(new Range("repair.plan"));
   MaskBits mb(hm, W);
@@ -1616,7 +1623,8 @@ static cel_status repair_bufs(cel_ctx* ctx, uint32_t k, bool own_eds, RepairBufs
   if (own_eds) b->eds = static_cast<uint8_t*>(scratch(ctx, S_EDS, eds_b, &e));
   b->dense[0] = static_cast<uint8_t*>(scratch(ctx, S_IN, 3 * eds_b, &e));
   b->tmp = static_cast<uint8_t*>(scratch(ctx, S_AUX, eds_b / 2 + (size_t)kIdxSlots * W * 4 + 256, &e));
-  b->mask = static_cast<uint8_t*>(scratch(ctx, S_MASK, 3 * cells_a, &e));
+  const size_t list_a = ((size_t)W * 4 + 255) & ~(size_t)255;
+  b->mask = static_cast<uint8_t*>(scratch(ctx, S_MASK, 3 * cells_a + list_a, &e));
   b->work = static_cast<uint8_t*>(scratch(ctx, S_WORK, nmt_workspace_size(k, 1), &e));
   const size_t roots_a = (2 * (size_t)W * kNode + 255) & ~(size_t)255;
   b->res_bytes = roots_a + 2 * (size_t)W * 4;
@@ -1625,12 +1633,14 @@ static cel_status repair_bufs(cel_ctx* ctx, uint32_t k, bool own_eds, RepairBufs
     return fail(ctx, CEL_ENOMEM, "device allocation failed");
   b->dense[1] = b->dense[0] + eds_b;
   b->dchk = b->dense[1] + eds_b;
-  b->dmask = b->mask + cells_a;
+  b->list0 = reinterpret_cast<int32_t*>(b->mask + cells_a);
+  b->dmask = b->mask + cells_a + list_a;
   b->dmask_chk = b->dmask + cells_a;
   b->flags = reinterpret_cast<int32_t*>(b->roots + roots_a);
   b->idx = reinterpret_cast<int32_t*>(b->tmp + eds_b / 2);
   const size_t cells_h = (cells + 255) & ~(size_t)255;
-  const size_t hb = (size_t)kIdxSlots * W * 4 + cells_h + b->res_bytes;  // axis lists, mask, results
+  // axis lists, mask + first list, results
+  const size_t hb = (size_t)kIdxSlots * W * 4 + cells_h + list_a + b->res_bytes;
   if (ctx->hstage_size < hb) {
     if (ctx->hstage) (void)hipHostFree(ctx->hstage);
     ctx->hstage = nullptr;
@@ -1641,7 +1651,7 @@ static cel_status repair_bufs(cel_ctx* ctx, uint32_t k, bool own_eds, RepairBufs
   }
   b->hidx = static_cast<int32_t*>(ctx->hstage);
   b->hmask = static_cast<uint8_t*>(ctx->hstage) + (size_t)kIdxSlots * W * 4;
-  b->hres = b->hmask + cells_h;
+  b->hres = b->hmask + cells_h + list_a;
   b->slot = 0;
   b->solves = 0;
   // the side stream and the events are the batch pipeline's (the ctx lock is held)
