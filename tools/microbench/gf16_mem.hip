@@ -142,8 +142,27 @@ static float run(const Geo& g, int reps) {
   return ms * 1e3f / reps;
 }
 
-int main() {
-  const size_t W = 1024, share = 512, pitch = W * share, eds = W * pitch;  // 512 MiB
+int main(int argc, char** argv) {
+  const size_t W = 1024, share = 512;
+  // argv[1] = "pad": the row pitch sweep (is the column pass's loss the 512 KiB stride?)
+  if (argc > 1) {
+    const size_t pads[] = {0, 256, 512, 2048, 4096, 8192 + 256};
+    for (size_t pad : pads) {
+      const size_t pitch = W * share + pad;
+      uint8_t* d;
+      CK(hipMalloc(&d, W * pitch));
+      CK(hipMemset(d, 1, W * pitch));
+      const Geo rows{d, d + 512 * share, share, (uint32_t)pitch, share, (uint32_t)pitch, 512};
+      const Geo cols{d, d + 512 * pitch, (uint32_t)pitch, share, (uint32_t)pitch, share, 1024};
+      const float r = run<8, 0>(rows, 5), c = run<8, 0>(cols, 5);
+      const float r2 = run<8, 54>(rows, 5), c2 = run<8, 54>(cols, 5);
+      printf("pitch pad %6zu B: map 8 rows %7.1f us cols %7.1f us (%5.2f TB/s); with filler rows %7.1f cols %7.1f us\n",
+             pad, r, c, 2.0 * 1024 * 512 * 512 / c / 1e6, r2, c2);
+      CK(hipFree(d));
+    }
+    return 0;
+  }
+  const size_t pitch = W * share, eds = W * pitch;  // 512 MiB
   uint8_t* d;
   CK(hipMalloc(&d, eds));
   CK(hipMemset(d, 1, eds));
