@@ -185,7 +185,13 @@ cel_status cel_device_name(cel_ctx* ctx, char* buf, size_t len) {
 // tree top + DAH runs beside the other's work. Two chunks (profiles/r1g_pipe_chunks_ab.txt);
 // chaining the extensions so each runs beside the previous chunk's hashing buys nothing,
 // the step is the sum of the two VALU-bound phases (profiles/r2_pipe_overlap_ab.txt).
-constexpr uint32_t kPipeChunks = 2;
+#ifndef CEL_PIPE_CHUNKS
+#define CEL_PIPE_CHUNKS 2
+#endif
+#ifndef CEL_PIPE_CHAIN
+#define CEL_PIPE_CHAIN 0
+#endif
+constexpr uint32_t kPipeChunks = CEL_PIPE_CHUNKS;
 
 static void pipe_plan(uint32_t n, uint32_t* chunk, uint32_t* nchunks) {
   uint32_t nc = n < kPipeChunks ? n : kPipeChunks;
@@ -286,6 +292,7 @@ cel_status cel_dev_extend_batch(cel_ctx* ctx, const void* d_ods, uint32_t n, uin
     const uint32_t first = c * chunk, cnt = (first + chunk <= n) ? chunk : n - first;
     hipStream_t s = ctx->sub[c % cel_ctx::kPipe];
     if ((e = hipStreamWaitEvent(s, ctx->ev_start, 0)) != hipSuccess) break;
+    if (CEL_PIPE_CHAIN && c > 0 && (e = hipStreamWaitEvent(s, ctx->ev_rs[c - 1], 0)) != hipSuccess) break;
     const uint8_t* ods = d_ods ? static_cast<const uint8_t*>(d_ods) + first * ods_sq : nullptr;
     uint8_t* eds = static_cast<uint8_t*>(d_eds) + first * eds_sq;
     if ((e = launch_extend(ods, eds, k, cnt, ctx->tables, s)) != hipSuccess) break;
