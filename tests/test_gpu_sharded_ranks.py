@@ -100,3 +100,50 @@ def test_rccl_one_rank_torchcomm(oracle, tmp_path):
     _, rr, cr, dah = oracle.extend_and_commit(random_ods(k, 78), want_eds=False)
     assert np.array_equal(got["rr"], rr) and np.array_equal(got["cr"], cr)
     assert got["dah"].tobytes() == dah
+
+
+def _worker_pipelined(rank, world, port, k, seeds, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch
+    import torch.distributed as dist
+    from celestia_eds import default_context
+    from celestia_eds.sharded import DeviceSteps, ShardedSquare, StagedComm, run_pipelined
+    from celestia_eds.testfactory import random_ods
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    ctx = default_context(0)
+    sqs = []
+    for sd in seeds:
+        sq = ShardedSquare(k, rank, world, DeviceSteps(ctx, 0))
+        lo, hi = sq.row_range()
+        sq.ods_rows.copy_(torch.from_numpy(np.ascontiguousarray(random_ods(k, sd)[lo:hi])))
+        sqs.append(sq)
+    for _ in range(2):  # the second round reuses every buffer
+        run_pipelined(sqs, StagedComm())
+    torch.cuda.synchronize()
+    for i, sq in enumerate(sqs):
+        sq.check_status()
+        np.savez(os.path.join(outdir, f"r{rank}_{i}.npz"), rr=sq.row_roots.cpu().numpy(),
+                 cr=sq.col_roots.cpu().numpy(), dah=sq.dah.cpu().numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_pipelined_squares(oracle, tmp_path):
+    """Two ranks (processes) with three row-sharded squares in flight each
+    (sharded.run_pipelined: own stream and workspace per square, the collectives of all
+    squares in one order on both ranks), device steps on the GPU, collectives over gloo
+    with host staging: every square's roots and DAH equal its whole-square oracle."""
+    import torch.multiprocessing as mp
+    from celestia_eds.testfactory import random_ods
+    k, world, seeds = 256, 2, (81, 82, 83)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_worker_pipelined, args=(world, port, k, seeds, str(tmp_path)), nprocs=world, join=True)
+    for i, sd in enumerate(seeds):
+        _, rr, cr, dah = oracle.extend_and_commit(random_ods(k, sd), want_eds=False)
+        for r in range(world):
+            got = np.load(tmp_path / f"r{r}_{i}.npz")
+            assert np.array_equal(got["rr"], rr) and np.array_equal(got["cr"], cr), (r, sd)
+            assert got["dah"].tobytes() == dah
