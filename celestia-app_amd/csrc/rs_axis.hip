@@ -55,6 +55,9 @@ constexpr uint32_t merged_lm(uint32_t s1, uint32_t s2) {
 #ifndef CEL_AX_SB
 #define CEL_AX_SB 1
 #endif
+#ifndef CEL_AX_LDS
+#define CEL_AX_LDS 0
+#endif
 template <int J>
 __device__ __forceinline__ void vperm_fence() {
   if constexpr (CEL_AX_SB > 0 && (J + 1) % (CEL_AX_SB > 0 ? CEL_AX_SB : 1) == 0) __builtin_amdgcn_sched_barrier(0);
@@ -190,7 +193,9 @@ hipError_t launch(const RsGeom& g, hipStream_t s) {
   const uint64_t ntiles = (uint64_t)g.axes * nslice * g.nsq;
   if (ntiles == 0) return hipSuccess;
   if (ntiles > 0xFFFFFFF0ull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_rs_axis_gf8<LOGK>, dim3((unsigned)((ntiles + 3) / 4)), dim3(256), 0, s, g, nslice);
+  // CEL_AX_LDS (A/B knob, default 0): dynamic LDS per workgroup that caps the RS
+  // workgroups per CU (160 KiB / CEL_AX_LDS), leaving register room for NMT waves beside them
+  hipLaunchKernelGGL(k_rs_axis_gf8<LOGK>, dim3((unsigned)((ntiles + 3) / 4)), dim3(256), CEL_AX_LDS, s, g, nslice);
   return hipGetLastError();
 }
 
