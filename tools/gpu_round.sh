@@ -1,10 +1,12 @@
 #!/bin/bash
-# One GPU-box pass: the -m gpu parity suite, then the default bench line and the repair
-# line. Every step has its own time limit; the chain stops at the first failure.
+# One GPU-box pass: smoke(), the -m gpu parity suite, then the default bench line and the
+# repair line. Every step has its own time limit; the chain stops at the first failure.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 tag=${1:-r2}
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${tag}_smoke.log 2>&1 || { tail -20 gpurun_out/${tag}_smoke.log; exit 1; }
+tail -1 gpurun_out/${tag}_smoke.log
 timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
   > gpurun_out/${tag}_pytest_gpu.log 2>&1
 rc=$?
