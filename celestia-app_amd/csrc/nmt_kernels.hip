@@ -258,6 +258,9 @@ __device__ __forceinline__ uint32_t node_word(const uint32_t (&L)[kNodeWords], c
   return 0u;
 }
 
+// UNR: blocks 1 and 2 with every round unrolled (latency-bound levels: a few waves per
+// SIMD, one node per lane, so the rolled loop's overhead sits on the chain).
+template <bool UNR = false>
 __device__ __forceinline__ void hash_node(const uint32_t (&L)[kNodeWords], const uint32_t (&R)[kNodeWords],
                                           uint32_t (&out)[kNodeWords]) {
   uint32_t st[8];
@@ -284,7 +287,8 @@ __device__ __forceinline__ void hash_node(const uint32_t (&L)[kNodeWords], const
     uint32_t w[16];
 #pragma unroll
     for (int wi = 0; wi < 16; wi++) w[wi] = node_word(L, R, 16 * b + wi);
-    sha256_compress(st, w);
+    if (UNR) sha256_compress_unrolled(st, w);
+    else sha256_compress(st, w);
   }
   bool rpar = (R[7] & 0xFFu) == 0xFFu;
 #pragma unroll
@@ -310,7 +314,7 @@ __device__ __forceinline__ void rfc_leaf90(const uint32_t (&R)[kNodeWords], uint
 // 90 bytes, straight into the caller's row_out / col_out ([nsq][W][90]); with
 // leafd != nullptr it also hashes the root as an RFC-6962 leaf of the DAH tree
 // (2 compressions) so the per-square DAH kernel starts from leaf digests.
-template <bool FROM_LEAVES>
+template <bool FROM_LEAVES, bool UNR = false>
 __global__ CEL_LEVEL_BOUNDS void k_level(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint32_t W,
                                                uint32_t nin, uint32_t trees, uint32_t* __restrict__ leafd,
                                                uint8_t* __restrict__ row_out, uint8_t* __restrict__ col_out) {
@@ -331,7 +335,7 @@ __global__ CEL_LEVEL_BOUNDS void k_level(const uint32_t* __restrict__ in, uint32
   uint32_t L[kNodeWords], R[kNodeWords], o[kNodeWords];
   load_node(in + li * kNodeWords, L);
   load_node(in + ri * kNodeWords, R);
-  hash_node(L, R, o);
+  hash_node<UNR>(L, R, o);
   const uint64_t oi = (uint64_t)blockIdx.y * trees * nout + idx;
   store_node(out + oi * kNodeWords, o);
   if (row_out) {
@@ -375,7 +379,12 @@ __device__ __forceinline__ void rfc_leaf90(const uint32_t (&R)[kNodeWords], uint
   }
 }
 
-// innerHash = SHA256(0x01 || l(32) || r(32)) (2 blocks).
+// innerHash = SHA256(0x01 || l(32) || r(32)) (2 blocks). The DAH tree hashes its levels
+// one after the other in one workgroup (a latency chain), so both compressions are
+// unrolled; the second block's 15 constant words fold into its schedule.
+#ifndef CEL_DAH_UNROLL
+#define CEL_DAH_UNROLL 0
+#endif
 __device__ __forceinline__ void rfc_inner(const uint32_t* l, const uint32_t* r, uint32_t (&st)[8]) {
   uint32_t w[16];
   w[0] = 0x01000000u | (l[0] >> 8);
@@ -385,13 +394,18 @@ __device__ __forceinline__ void rfc_inner(const uint32_t* l, const uint32_t* r, 
 #pragma unroll
   for (int i = 9; i < 16; i++) w[i] = __builtin_amdgcn_alignbit(r[i - 9], r[i - 8], 8);
   sha256_init(st);
-  sha256_compress(st, w);
   uint32_t w2[16];
   w2[0] = (r[7] << 24) | 0x00800000u;
 #pragma unroll
   for (int i = 1; i < 15; i++) w2[i] = 0;
   w2[15] = 65u * 8u;
-  sha256_compress(st, w2);
+  if (CEL_DAH_UNROLL) {
+    sha256_compress_unrolled(st, w);
+    sha256_compress_unrolled(st, w2);
+  } else {
+    sha256_compress(st, w);
+    sha256_compress(st, w2);
+  }
 }
 
 // SHA256 of the empty string (RFC-6962 empty tree).
@@ -509,6 +523,11 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // latency is then exposed and the prefetching leaf hash (leaf_hash<true>) pays.
 static bool latency_bound(uint64_t lanes) { return lanes <= 2ull * 1024 * 64; }
 
+// Tree levels of at most latency_bound() lanes hash with unrolled compressions (A/B knob).
+#ifndef CEL_LEVEL_UNROLL
+#define CEL_LEVEL_UNROLL 0
+#endif
+
 // Workspace: leaves [nsq][W*W] nodes | ping [nsq][2W][W/2] | pong [nsq][2W][W/4] |
 //            roots [nsq][2W] nodes | bad_axis [nsq] int32 | DAH leaf digests [nsq][2W][8]
 size_t nmt_workspace_size(uint32_t k, uint32_t nsq) {
@@ -563,8 +582,10 @@ hipError_t launch_commit(const uint8_t* eds, uint32_t k, uint32_t nsq, uint8_t* 
     dim3 g((trees * nout + 255) / 256, nsq);
     uint8_t* ro = (nout == 1) ? row_roots : nullptr;
     uint8_t* co = (nout == 1) ? col_roots : nullptr;
+    const bool unr = CEL_LEVEL_UNROLL && latency_bound((uint64_t)trees * nout * nsq);
     if (first) hipLaunchKernelGGL(k_level<true>, g, dim3(256), 0, s, src, out, W, nin, trees, ld, ro, co);
-    else hipLaunchKernelGGL(k_level<false>, g, dim3(256), 0, s, src, out, W, nin, trees, ld, ro, co);
+    else if (unr) hipLaunchKernelGGL((k_level<false, true>), g, dim3(256), 0, s, src, out, W, nin, trees, ld, ro, co);
+    else hipLaunchKernelGGL((k_level<false, false>), g, dim3(256), 0, s, src, out, W, nin, trees, ld, ro, co);
     first = false;
     src = out;
     dst = (dst == ping) ? pong : ping;
@@ -632,6 +653,7 @@ struct LevelJob {
   uint32_t nin, trees, tstride, lstride;
 };
 
+template <bool UNR>
 __global__ CEL_LEVEL_BOUNDS void k_level_pair(LevelJob a, LevelJob b) {
   uint32_t idx = blockIdx.x * 256u + threadIdx.x;
   const uint32_t na = a.nin > 1 ? a.trees * (a.nin / 2) : 0u;
@@ -645,7 +667,7 @@ __global__ CEL_LEVEL_BOUNDS void k_level_pair(LevelJob a, LevelJob b) {
   uint32_t L[kNodeWords], R[kNodeWords], o[kNodeWords];
   load_node(j.in + li * kNodeWords, L);
   load_node(j.in + ri * kNodeWords, R);
-  hash_node(L, R, o);
+  hash_node<UNR>(L, R, o);
   store_node(j.out + (uint64_t)idx * kNodeWords, o);
 }
 
@@ -726,7 +748,8 @@ static void reduce_grid_pair(LevelJob a, uint32_t* ping_a, uint32_t* pong_a, uin
     if (a.nin > 1) a.out = a.nin == 2 ? roots_a : dst_a;
     if (b.nin > 1) b.out = b.nin == 2 ? roots_b : dst_b;
     const uint32_t n = (a.nin > 1 ? a.trees * (a.nin / 2) : 0u) + (b.nin > 1 ? b.trees * (b.nin / 2) : 0u);
-    hipLaunchKernelGGL(k_level_pair, dim3((n + 255) / 256), dim3(256), 0, s, a, b);
+    if (CEL_LEVEL_UNROLL && latency_bound(n)) hipLaunchKernelGGL(k_level_pair<true>, dim3((n + 255) / 256), dim3(256), 0, s, a, b);
+    else hipLaunchKernelGGL(k_level_pair<false>, dim3((n + 255) / 256), dim3(256), 0, s, a, b);
     if (a.nin > 1) {
       a.in = a.out;
       a.nin /= 2;

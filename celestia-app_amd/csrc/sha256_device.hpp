@@ -87,6 +87,27 @@ __device__ __forceinline__ void sha256_compress(uint32_t (&st)[8], uint32_t (&w)
   sha256_compress_from<0>(st, ShaRegs{st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7]}, w);
 }
 
+// The same compression with all 64 rounds unrolled: for latency-bound kernels (one wave
+// per SIMD, a serial chain of compressions), where a rolled loop's overhead is on the
+// chain and message words known at compile time (padding blocks) fold into the schedule.
+__device__ __forceinline__ void sha256_compress_unrolled(uint32_t (&st)[8], uint32_t (&w)[16]) {
+  ShaRegs r{st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7]};
+#pragma unroll
+  for (int i = 0; i < 16; i++) sha_round(r, w[i] + kSha256K[i]);
+#pragma unroll
+  for (int i = 16; i < 64; i++) {
+    const int j = i & 15;
+    const uint32_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
+    const uint32_t s0 = xor3(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
+    const uint32_t s1 = xor3(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
+    const uint32_t wi = w[j] + s0 + w[(j + 9) & 15] + s1;
+    w[j] = wi;
+    sha_round(r, wi + kSha256K[i]);
+  }
+  st[0] += r.a; st[1] += r.b; st[2] += r.c; st[3] += r.d;
+  st[4] += r.e; st[5] += r.f; st[6] += r.g; st[7] += r.h;
+}
+
 // Compile-time SHA-256: working variables after the first n rounds of a first block
 // (chaining value = IV) whose words w[0..n) are constants. Used for the constant
 // prefixes of parity leaves (0x00 || 0xFF*27...) and parity inner nodes (0x01 || 0xFF*55).
