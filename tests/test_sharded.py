@@ -197,3 +197,24 @@ def test_device_pipelined_one_rank(ctx, oracle):
         assert np.array_equal(sq.slab.cpu().numpy(), eds)
         assert np.array_equal(sq.row_roots.cpu().numpy(), rr) and np.array_equal(sq.col_roots.cpu().numpy(), cr)
         assert sq.dah.cpu().numpy().tobytes() == dah
+
+
+def test_pipelined_one_rank_oracle(oracle):
+    """run_pipelined without collectives (one rank): the record block is copied into the
+    gathered buffer in place of the all-gather; two squares in flight, each equals its
+    whole-square oracle (CPU, oracle-backed steps)."""
+    from celestia_eds.sharded import ShardedSquare, run_pipelined
+    from sharded_oracle import OracleSteps
+    k, seeds = 8, (91, 92)
+    sqs = []
+    for sd in seeds:
+        sq = ShardedSquare(k, 0, 1, OracleSteps())
+        sq.ods_rows.copy_(torch.from_numpy(random_ods(k, sd)))
+        sqs.append(sq)
+    run_pipelined(sqs, None)
+    for sd, sq in zip(seeds, sqs):
+        eds, rr, cr, dah = oracle.extend_and_commit(random_ods(k, sd))
+        assert int(sq.status.item()) == 0
+        assert np.array_equal(sq.slab.numpy(), eds)
+        assert np.array_equal(sq.row_roots.numpy(), rr) and np.array_equal(sq.col_roots.numpy(), cr)
+        assert sq.dah.numpy().tobytes() == dah
