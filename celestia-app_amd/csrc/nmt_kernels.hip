@@ -671,41 +671,60 @@ __global__ CEL_LEVEL_BOUNDS void k_level_pair(LevelJob a, LevelJob b) {
   store_node(j.out + (uint64_t)idx * kNodeWords, o);
 }
 
-// Push order across slab boundaries (rows of Q0): the last leaf of slab r-1 must not
-// carry a larger namespace than the first leaf of slab r. Within a sorted slab those are
-// the subtree's maxNs and minNs. subs: rank r's 2k row-subtree records at subs[r * stride].
-__global__ void k_slab_boundary(const uint32_t* __restrict__ subs, uint32_t k, uint32_t w, uint32_t nranks,
-                                uint32_t stride, int32_t* __restrict__ bad_axis) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= k) return;
-  for (uint32_t r = 1; r < nranks && r * w < k; r++) {
-    const uint8_t* L = reinterpret_cast<const uint8_t*>(subs + ((uint64_t)(r - 1) * stride + i) * kNodeWords);
-    const uint8_t* R = reinterpret_cast<const uint8_t*>(subs + ((uint64_t)r * stride + i) * kNodeWords);
-    for (uint32_t b = 0; b < kNs; b++) {
-      const uint8_t lm = L[kNs + b], rm = R[b];
-      if (lm != rm) {
-        if (rm < lm) atomicMin(bad_axis, (int32_t)i);
-        break;
-      }
-    }
+// Namespace compare of two node records: is R's minNs (bytes 0..28) below L's maxNs
+// (bytes 29..57)? Big-endian words: 7 full words, then the 29th byte.
+__device__ __forceinline__ bool min_below_max(const uint32_t* __restrict__ R, const uint32_t* __restrict__ L) {
+  uint32_t r[8], l[16];
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const uint4 v = reinterpret_cast<const uint4*>(R)[q];
+    r[4 * q] = v.x; r[4 * q + 1] = v.y; r[4 * q + 2] = v.z; r[4 * q + 3] = v.w;
   }
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const uint4 v = reinterpret_cast<const uint4*>(L)[q];
+    l[4 * q] = v.x; l[4 * q + 1] = v.y; l[4 * q + 2] = v.z; l[4 * q + 3] = v.w;
+  }
+#pragma unroll
+  for (int q = 0; q < 7; q++) {
+    const uint32_t a = bswap32(r[q]), b = bswap32(__builtin_amdgcn_alignbyte(l[8 + q], l[7 + q], 1));
+    if (a != b) return a < b;
+  }
+  return (r[7] & 0xFFu) < ((l[14] >> 8) & 0xFFu);
 }
 
-// status = max over the nranks gathered step-2 status records (first int32 of record
-// r * stride + at).
-__global__ void k_status_max(const uint32_t* __restrict__ gathered, uint32_t stride, uint32_t at, uint32_t nranks,
-                             int32_t* __restrict__ status) {
-  if (threadIdx.x != 0) return;
-  int32_t m = 0;
-  for (uint32_t r = 0; r < nranks; r++) {
-    const int32_t v = (int32_t)gathered[((uint64_t)r * stride + at) * kNodeWords];
-    m = v > m ? v : m;
+// The finish's status in one workgroup: the max over ranks of the gathered step-2 status
+// (first int32 of record r * stride + at), or CEL_EORDER when the push order breaks
+// across a slab boundary in a row of Q0 (rank r's first leaf namespace below rank r-1's
+// last: the subtrees' minNs / maxNs; subs: rank r's 2k row-subtree records at
+// subs[r * stride]).
+__global__ __launch_bounds__(256) void k_shard_status(const uint32_t* __restrict__ subs, uint32_t stride, uint32_t at,
+                                                      uint32_t k, uint32_t w, uint32_t nranks, int order_check,
+                                                      int32_t* __restrict__ status) {
+  __shared__ int bad;
+  if (threadIdx.x == 0) bad = 0;
+  __syncthreads();
+  if (order_check) {
+    int mine = 0;
+    for (uint32_t i = threadIdx.x; i < k; i += blockDim.x)
+      for (uint32_t r = 1; r < nranks && r * w < k; r++)
+        mine |= min_below_max(subs + ((uint64_t)r * stride + i) * kNodeWords,
+                              subs + ((uint64_t)(r - 1) * stride + i) * kNodeWords);
+    if (mine) atomicOr(&bad, 1);
   }
-  *status = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int32_t m = 0;
+    for (uint32_t r = 0; r < nranks; r++) {
+      const int32_t v = (int32_t)subs[((uint64_t)r * stride + at) * kNodeWords];
+      m = v > m ? v : m;
+    }
+    *status = bad ? CEL_EORDER : m;
+  }
 }
 
 __global__ void k_status_from_bad(const int32_t* __restrict__ bad_axis, int32_t* __restrict__ status) {
-  if (threadIdx.x == 0 && *bad_axis != INT_MAX) *status = CEL_EORDER;
+  if (threadIdx.x == 0) *status = *bad_axis != INT_MAX ? CEL_EORDER : CEL_OK;
 }
 
 __global__ void k_pack_records(const uint32_t* __restrict__ rec, uint32_t n, uint8_t* __restrict__ out) {
@@ -792,7 +811,6 @@ hipError_t launch_slab_commit(const uint8_t* slab, uint32_t k, uint32_t c0, uint
   base += align256((size_t)k * w * nb + nb);
   uint32_t* pong2 = reinterpret_cast<uint32_t*>(base);
   hipLaunchKernelGGL(k_fill_i32, dim3(1), dim3(64), 0, s, bad, 1u, INT_MAX);
-  hipLaunchKernelGGL(k_fill_i32, dim3(1), dim3(64), 0, s, status, 1u, 0);
   dim3 gl((W * w + 255) / 256);
   if (latency_bound(W * w)) {
     if (order_check) hipLaunchKernelGGL((k_slab_leaf<true, true>), gl, dim3(256), 0, s, slab, k, c0, w, leaves, bad);
@@ -814,7 +832,7 @@ hipError_t launch_slab_commit(const uint8_t* slab, uint32_t k, uint32_t c0, uint
   return hipGetLastError();
 }
 
-// Workspace: ping/pong [2k * nranks / 2] | items [4k] | bad | DAH leaf digests [4k][8]
+// Workspace: ping/pong [2k * nranks / 2] | items [4k] | (256 B unused) | DAH leaf digests [4k][8]
 size_t shard_finish_workspace_size(uint32_t k, uint32_t nranks) {
   const size_t nb = kNodeWords * 4, W = 2 * (size_t)k;
   return 2 * align256(W * (nranks / 2 + 1) * nb) + align256(2 * W * nb) + 256 + align256(2 * W * 32);
@@ -833,13 +851,11 @@ hipError_t launch_shard_finish(const uint32_t* gathered, uint32_t k, uint32_t nr
   uint32_t* pong = reinterpret_cast<uint32_t*>(base);
   base += align256((size_t)W * (nranks / 2 + 1) * nb);
   uint32_t* items = reinterpret_cast<uint32_t*>(base);  // [rows 2k | cols 2k]
-  base += align256((size_t)2 * W * nb);
-  int32_t* bad = reinterpret_cast<int32_t*>(base);
-  base += 256;
+  base += align256((size_t)2 * W * nb) + 256;
   uint32_t* leafd = reinterpret_cast<uint32_t*>(base);
-  hipLaunchKernelGGL(k_fill_i32, dim3(1), dim3(64), 0, s, bad, 1u, INT_MAX);
-  if (order_check && nranks > 1)
-    hipLaunchKernelGGL(k_slab_boundary, dim3((k + 255) / 256), dim3(256), 0, s, row_subs, k, w, nranks, S, bad);
+  // the ranks' step-2 status (max), or EORDER across slab boundaries: one workgroup
+  hipLaunchKernelGGL(k_shard_status, dim3(1), dim3(256), 0, s, gathered, S, W + w, k, w, nranks,
+                     (order_check && nranks > 1) ? 1 : 0, status);
   // row i's subtree from rank r is gathered[r][i]: trees of nranks leaves, stride S
   hipError_t e = hipSuccess;
   if (nranks == 1) e = hipMemcpyAsync(items, row_subs, (size_t)W * nb, hipMemcpyDeviceToDevice, s);
@@ -849,9 +865,6 @@ hipError_t launch_shard_finish(const uint32_t* gathered, uint32_t k, uint32_t nr
     e = hipMemcpy2DAsync(items + (size_t)W * kNodeWords, (size_t)w * nb, gathered + (size_t)W * kNodeWords,
                          (size_t)S * nb, (size_t)w * nb, nranks, hipMemcpyDeviceToDevice, s);
   if (e != hipSuccess) return e;
-  // the ranks' step-2 status (max), then the push order across slab boundaries
-  hipLaunchKernelGGL(k_status_max, dim3(1), dim3(64), 0, s, gathered, S, W + w, nranks, status);
-  hipLaunchKernelGGL(k_status_from_bad, dim3(1), dim3(64), 0, s, bad, status);
   // the 4k RFC-6962 leaf digests and the packed roots one lane each, then the DAH tree
   // one level per round in one workgroup
   hipLaunchKernelGGL(k_dah_leaves, dim3((2 * W + 255) / 256), dim3(256), 0, s, items, 2 * W, leafd, row_roots,

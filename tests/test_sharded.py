@@ -218,3 +218,26 @@ def test_pipelined_one_rank_oracle(oracle):
         assert np.array_equal(sq.slab.numpy(), eds)
         assert np.array_equal(sq.row_roots.numpy(), rr) and np.array_equal(sq.col_roots.numpy(), cr)
         assert sq.dah.numpy().tobytes() == dah
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_device_sharded_order_across_slabs(ctx, oracle, n):
+    """Each row's two column halves swapped: columns stay sorted and, for n >= 4, every slab
+    of Q0 is sorted inside, so the push-order break is only across slab boundaries (the
+    finish's check of subtree minNs against the previous slab's maxNs); n = 2 catches it
+    inside the slab. Every rank reports EORDER, like the whole-square check."""
+    from celestia_eds import _lib
+    from celestia_eds.sharded import DeviceSteps, LocalComm, ShardedSquare
+    k = 256
+    ods = random_ods(k, 700 + n)
+    ods = np.concatenate([ods[:, k // 2:], ods[:, :k // 2]], axis=1).copy()
+    assert oracle.roots(oracle.extend(ods), check_order=True)[0] != 0  # the oracle sees the break too
+    steps = DeviceSteps(ctx)
+    squares = [ShardedSquare(k, r, n, steps) for r in range(n)]
+    for s in squares:
+        a, b = s.row_range()
+        s.ods_rows.copy_(torch.from_numpy(np.ascontiguousarray(ods[a:b])))
+    LocalComm.run(squares)
+    steps.stream.synchronize()
+    assert all(int(s.status.item()) == _lib.EORDER for s in squares)
