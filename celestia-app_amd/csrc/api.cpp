@@ -500,11 +500,16 @@ cel_status cel_dev_shard_cols(cel_ctx* ctx, void* d_slab, uint32_t k, uint32_t n
   gm.len = kShare;
   gm.axes = w;
   gm.nsq = 1;
-  hipError_t e = launch_rs_encode(gm, ctx->tables, s);
-  if (e != hipSuccess) return hip_fail(ctx, e, "shard cols");
-  e = launch_slab_commit(slab, k, rank * w, w, static_cast<uint32_t*>(d_col_rec), static_cast<uint32_t*>(d_row_sub),
-                         d_status, d_work, (flags & CEL_FLAG_ORDER_CHECK) != 0, s);
-  return e == hipSuccess ? CEL_OK : hip_fail(ctx, e, "shard commit");
+  // Column pass, then the slab's leaves and trees. Hashing the top half's leaves on a
+  // second stream beside the column pass measured no faster (profiles/r3_rank_latency.txt).
+  const bool order = (flags & CEL_FLAG_ORDER_CHECK) != 0;
+  hipError_t e;
+  if ((e = launch_rs_encode(gm, ctx->tables, s)) != hipSuccess) return hip_fail(ctx, e, "shard cols");
+  if ((e = launch_slab_leaves(slab, k, rank * w, w, 0, 2 * k, d_work, order, true, s)) != hipSuccess ||
+      (e = launch_slab_trees(k, w, static_cast<uint32_t*>(d_col_rec), static_cast<uint32_t*>(d_row_sub), d_status,
+                             d_work, s)) != hipSuccess)
+    return hip_fail(ctx, e, "shard commit");
+  return CEL_OK;
 }
 
 cel_status cel_dev_shard_finish(cel_ctx* ctx, const void* d_gathered, uint32_t k, uint32_t nranks, void* d_row_roots,

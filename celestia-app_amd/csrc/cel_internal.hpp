@@ -113,8 +113,12 @@ size_t slices_workspace_size(uint32_t n);
 
 // Row-sharded mode (one column slab of one square per rank).
 size_t slab_workspace_size(uint32_t k, uint32_t w);
-hipError_t launch_slab_commit(const uint8_t* slab, uint32_t k, uint32_t c0, uint32_t w, uint32_t* col_rec,
-                              uint32_t* row_sub, int32_t* status, void* work, bool order_check, hipStream_t s);
+// The slab commit in two steps: leaves of slab rows [row0, row1) (the rows < k half first,
+// init_bad resetting the push-order flag), then, after every leaf, the trees and status.
+hipError_t launch_slab_leaves(const uint8_t* slab, uint32_t k, uint32_t c0, uint32_t w, uint32_t row0, uint32_t row1,
+                              void* work, bool order_check, bool init_bad, hipStream_t s);
+hipError_t launch_slab_trees(uint32_t k, uint32_t w, uint32_t* col_rec, uint32_t* row_sub, int32_t* status,
+                             void* work, hipStream_t s);
 size_t shard_finish_workspace_size(uint32_t k, uint32_t nranks);
 // gathered: [nranks][2k + w + 1] records, rank order (row subtrees, column roots, status).
 hipError_t launch_shard_finish(const uint32_t* gathered, uint32_t k, uint32_t nranks, uint8_t* row_roots,

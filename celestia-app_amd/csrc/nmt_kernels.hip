@@ -612,10 +612,11 @@ hipError_t launch_commit(const uint8_t* eds, uint32_t k, uint32_t nsq, uint8_t* 
 
 template <bool ORDER, bool PF>
 __global__ CEL_LEAF_BOUNDS void k_slab_leaf(const uint8_t* __restrict__ slab, uint32_t k, uint32_t c0, uint32_t w,
-                                            uint32_t* __restrict__ leaves, int32_t* __restrict__ bad_axis) {
+                                            uint32_t cell0, uint32_t cell1, uint32_t* __restrict__ leaves,
+                                            int32_t* __restrict__ bad_axis) {
   const uint32_t W = 2 * k;
-  const uint32_t cell = blockIdx.x * 256u + threadIdx.x;
-  if (cell >= W * w) return;
+  const uint32_t cell = cell0 + blockIdx.x * 256u + threadIdx.x;
+  if (cell >= cell1) return;
   const uint32_t i = cell / w, j = cell % w, c = c0 + j;
   const uint32_t* sh = reinterpret_cast<const uint32_t*>(slab + (uint64_t)cell * kShare);
   const bool q0 = (i < k) && (c < k);
@@ -793,42 +794,72 @@ size_t slab_workspace_size(uint32_t k, uint32_t w) {
   return align256(W * w * nb) + 4 * align256((size_t)k * w * nb + nb) + align256(W * 2 * nb) + 256;
 }
 
-hipError_t launch_slab_commit(const uint8_t* slab, uint32_t k, uint32_t c0, uint32_t w, uint32_t* col_rec,
-                              uint32_t* row_sub, int32_t* status, void* work, bool order_check, hipStream_t s) {
+// The slab commit's workspace: leaves, the column trees' ping / pong, the roots area, the
+// order flag, the row subtrees' ping / pong.
+struct SlabWork {
+  uint32_t *leaves, *ping, *pong, *ping2, *pong2;
+  int32_t* bad;
+};
+static SlabWork slab_work(void* work, uint32_t k, uint32_t w) {
   const uint32_t W = 2 * k;
   const size_t nb = kNodeWords * 4;
   uint8_t* base = static_cast<uint8_t*>(work);
-  uint32_t* leaves = reinterpret_cast<uint32_t*>(base);
+  SlabWork sw;
+  sw.leaves = reinterpret_cast<uint32_t*>(base);
   base += align256((size_t)W * w * nb);
-  uint32_t* ping = reinterpret_cast<uint32_t*>(base);
+  sw.ping = reinterpret_cast<uint32_t*>(base);
   base += align256((size_t)k * w * nb + nb);
-  uint32_t* pong = reinterpret_cast<uint32_t*>(base);
+  sw.pong = reinterpret_cast<uint32_t*>(base);
   base += align256((size_t)k * w * nb + nb);
   base += align256((size_t)W * 2 * nb);
-  int32_t* bad = reinterpret_cast<int32_t*>(base);
+  sw.bad = reinterpret_cast<int32_t*>(base);
   base += 256;
-  uint32_t* ping2 = reinterpret_cast<uint32_t*>(base);
+  sw.ping2 = reinterpret_cast<uint32_t*>(base);
   base += align256((size_t)k * w * nb + nb);
-  uint32_t* pong2 = reinterpret_cast<uint32_t*>(base);
-  hipLaunchKernelGGL(k_fill_i32, dim3(1), dim3(64), 0, s, bad, 1u, INT_MAX);
-  dim3 gl((W * w + 255) / 256);
-  if (latency_bound(W * w)) {
-    if (order_check) hipLaunchKernelGGL((k_slab_leaf<true, true>), gl, dim3(256), 0, s, slab, k, c0, w, leaves, bad);
-    else hipLaunchKernelGGL((k_slab_leaf<false, true>), gl, dim3(256), 0, s, slab, k, c0, w, leaves, bad);
+  sw.pong2 = reinterpret_cast<uint32_t*>(base);
+  return sw;
+}
+
+// Leaves of slab rows [row0, row1) (2k rows of w cells). The half holding rows < k checks
+// the push order and must come first in stream order after the flag is reset (init_bad).
+hipError_t launch_slab_leaves(const uint8_t* slab, uint32_t k, uint32_t c0, uint32_t w, uint32_t row0, uint32_t row1,
+                              void* work, bool order_check, bool init_bad, hipStream_t s) {
+  const SlabWork sw = slab_work(work, k, w);
+  if (init_bad) hipLaunchKernelGGL(k_fill_i32, dim3(1), dim3(64), 0, s, sw.bad, 1u, INT_MAX);
+  const uint32_t cell0 = row0 * w, cell1 = row1 * w;
+  if (cell1 <= cell0) return hipGetLastError();
+  dim3 gl((cell1 - cell0 + 255) / 256);
+  if (latency_bound(2ull * k * w)) {
+    if (order_check)
+      hipLaunchKernelGGL((k_slab_leaf<true, true>), gl, dim3(256), 0, s, slab, k, c0, w, cell0, cell1, sw.leaves, sw.bad);
+    else
+      hipLaunchKernelGGL((k_slab_leaf<false, true>), gl, dim3(256), 0, s, slab, k, c0, w, cell0, cell1, sw.leaves, sw.bad);
   } else {
-    if (order_check) hipLaunchKernelGGL((k_slab_leaf<true, false>), gl, dim3(256), 0, s, slab, k, c0, w, leaves, bad);
-    else hipLaunchKernelGGL((k_slab_leaf<false, false>), gl, dim3(256), 0, s, slab, k, c0, w, leaves, bad);
+    if (order_check)
+      hipLaunchKernelGGL((k_slab_leaf<true, false>), gl, dim3(256), 0, s, slab, k, c0, w, cell0, cell1, sw.leaves, sw.bad);
+    else
+      hipLaunchKernelGGL((k_slab_leaf<false, false>), gl, dim3(256), 0, s, slab, k, c0, w, cell0, cell1, sw.leaves,
+                         sw.bad);
   }
-  // w column trees of 2k leaves (leaf i of column j at i*w + j) and 2k row subtrees of w
-  // leaves (leaf j of row i at i*w + j), both sets one level per launch
+  return hipGetLastError();
+}
+
+// After every leaf of the slab: w column trees of 2k leaves (leaf i of column j at
+// i*w + j) and 2k row subtrees of w leaves (leaf j of row i at i*w + j), both sets one
+// level per launch, then the status.
+hipError_t launch_slab_trees(uint32_t k, uint32_t w, uint32_t* col_rec, uint32_t* row_sub, int32_t* status,
+                             void* work, hipStream_t s) {
+  const uint32_t W = 2 * k;
+  const size_t nb = kNodeWords * 4;
+  const SlabWork sw = slab_work(work, k, w);
   if (w == 1) {
-    const hipError_t e = hipMemcpyAsync(row_sub, leaves, (size_t)W * nb, hipMemcpyDeviceToDevice, s);
+    const hipError_t e = hipMemcpyAsync(row_sub, sw.leaves, (size_t)W * nb, hipMemcpyDeviceToDevice, s);
     if (e != hipSuccess) return e;
   }
-  const LevelJob cols{leaves, nullptr, W, w, 1, w};
-  const LevelJob rows{leaves, nullptr, w, W, w, 1};
-  reduce_grid_pair(cols, ping, pong, col_rec, rows, ping2, pong2, row_sub, s);
-  hipLaunchKernelGGL(k_status_from_bad, dim3(1), dim3(64), 0, s, bad, status);
+  const LevelJob cols{sw.leaves, nullptr, W, w, 1, w};
+  const LevelJob rows{sw.leaves, nullptr, w, W, w, 1};
+  reduce_grid_pair(cols, sw.ping, sw.pong, col_rec, rows, sw.ping2, sw.pong2, row_sub, s);
+  hipLaunchKernelGGL(k_status_from_bad, dim3(1), dim3(64), 0, s, sw.bad, status);
   return hipGetLastError();
 }
 
