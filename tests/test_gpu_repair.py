@@ -81,6 +81,22 @@ def test_gf16_repair_k256(ctx, oracle):
     assert np.array_equal(repair(ctx, eds, present, rr, cr), eds)
 
 
+def test_gf16_repair_k512(ctx, oracle):
+    """The largest square the device repairs: k = 512 (GF(2^16), 1024-shard axes through
+    gather -> LDS decoder -> scatter, 512 MiB EDS), Q0 only and a random p = 0.55 mask;
+    the repaired square is the original (the codeword is unique)."""
+    from celestia_eds import _lib
+    k = 512
+    eds, rr, cr = setup(oracle, k, seed=12)
+    w = 2 * k
+    q0 = np.zeros((w, w), np.uint8)
+    q0[:k, :k] = 1
+    rnd = (np.random.default_rng(12).random((w, w)) < 0.55).astype(np.uint8)
+    for present in (q0, rnd):
+        st, cells, _ = _dev_repair(ctx, eds, present, rr, cr)
+        assert st == _lib.OK and np.array_equal(cells, eds)
+
+
 def _dev_repair(ctx, eds, present, rr, cr, want_shares=False):
     """cel_dev_repair over a device-resident damaged copy; returns (status, cells, bad)
     (+ (byz_shares, byz_present, mask after) with want_shares)."""
