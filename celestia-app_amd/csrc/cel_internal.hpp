@@ -50,6 +50,7 @@ struct DeviceTables {
   uint16_t* log16 = nullptr;   // [65536]
   uint16_t* skew16 = nullptr;  // [65535]
   uint32_t* mul8 = nullptr;    // [256][8] GF(2^8) product tables indexed by log value (decoder)
+  uint32_t* tw16 = nullptr;    // [2047][8] GF(2^16) basis products c*(1 << i) of twiddle skew[s] (decoder)
 };
 
 // roctx range over a phase's launches (rocprofv3 --marker-trace shows them on the host
@@ -156,6 +157,10 @@ hipError_t launch_commitment(const uint8_t* d_cells, uint32_t k, uint32_t r0, ui
 
 // Erasure decode of `naxes` axes of 2n shards each, gathered into a dense
 // [naxes][2n][len] buffer with a [naxes][2n] present mask. In place.
+// GF(2^16) erasure decode over n = 512, 1024 or 2048 points (rs_decode_gf16.hip).
+bool rs_decode_gf16_supported(uint32_t n);
+hipError_t launch_rs_decode_gf16(uint8_t* shards, const uint8_t* present, uint32_t naxes, uint32_t n, uint32_t len,
+                                 const DeviceTables& t, hipStream_t s);
 hipError_t launch_rs_decode(uint8_t* shards, const uint8_t* present, uint32_t naxes, uint32_t n,
                             uint32_t len, const DeviceTables& t, void* work, hipStream_t s);
 size_t decode_workspace_size(uint32_t naxes, uint32_t n);

@@ -1,0 +1,293 @@
+// Leopard GF(2^16) erasure decode (2m = 512, 1024, 2048 points) in bit planes.
+//
+// Replaces klauspost/reedsolomon v1.12.1 leopard.go Reconstruct (catid/leopard's
+// ReedSolomonDecode) as rsmt2d v0.14.0 LeoRSCodec.Decode drives it above 256 shards
+// (pkg/appconsts/global_consts.go:92). Same decoder as
+// rs_kernels.hip's header: error locator by FWHT, scale, IFFT over all n points at offset
+// 0, formal derivative, FFT, unscale the erased points.
+//
+// Products. A 64-byte Leopard block holds 32 symbols, lo bytes in dwords 0-7 and hi bytes
+// in dwords 8-15. An 8x8 bit transpose in each byte lane (bs::tr8) turns each half into 8
+// bit planes: plane i (i < 8 from the lo half, 8 + (i - 8) from the hi half) holds bit i
+// of the 32 symbols' Cantor representations. Multiplying by a constant c is GF(2)-linear:
+// plane j of c*y is the xor of the planes i of y whose basis product P_i = c*(1 << i) has
+// bit j set, 16x16 masked xors (one v_bfe + one v_bitop3 each). The basis products of
+// every twiddle come from a 64 KiB table built on the host (DeviceTables::tw16); those of
+// the per-point scales (exp(+-err)) from the exp/log tables, once per workgroup.
+//
+// The previous LDS decoder looked every symbol's log and exp up in the 128 KiB global
+// tables (two gathers per product): k=512 repair's 1024-axis row pass took 16.2 ms,
+// L2-bound on the gathers (profiles/r3_bench_repair_k512.json).
+//
+// Layout: one workgroup per (axis, chunk set), n/2 threads (one butterfly each per layer),
+// the chunk's 16 planes of every point in LDS plane-major (plane j of point p at
+// [j * n + p]: consecutive lanes read consecutive words).
+#include <hip/hip_runtime.h>
+
+#include "bitslice8.hpp"
+#include "cel_internal.hpp"
+#include "leopard_field.hpp"
+
+namespace cel {
+
+namespace {
+
+constexpr uint32_t kMod16 = 65535u;
+
+// x ^= c*y (32 symbols, bit planes); pk[i / 2] half i % 2 holds P_i = c * (1 << i).
+// SUB: c lies in the subfield GF(2^8) (Cantor representation < 256), so P_i < 256 for
+// i < 8 and those rows never reach the hi planes.
+template <bool SUB>
+__device__ __forceinline__ void mul_acc(uint32_t (&x)[16], const uint32_t (&y)[16], const uint32_t (&pk)[8]) {
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      if (SUB && i < 8 && j >= 8) continue;
+      const uint32_t msk = (uint32_t)__builtin_amdgcn_sbfe((int)pk[i >> 1], 16 * (i & 1) + j, 1);
+      x[j] = __builtin_amdgcn_bitop3_b32(x[j], msk, y[i], 0x78);  // x ^ (msk & y)
+    }
+  }
+}
+
+__device__ __forceinline__ void load_tw(uint32_t (&pk)[8], const uint32_t* __restrict__ tw, uint32_t s) {
+  const uint4 a = reinterpret_cast<const uint4*>(tw)[2 * s];
+  const uint4 b = reinterpret_cast<const uint4*>(tw)[2 * s + 1];
+  pk[0] = a.x; pk[1] = a.y; pk[2] = a.z; pk[3] = a.w;
+  pk[4] = b.x; pk[5] = b.y; pk[6] = b.z; pk[7] = b.w;
+}
+
+// Basis products of exp(e): P_b = exp[log[1 << b] + e] (e < 65535; a partial reduction
+// may give 65535, and exp[65535] = exp[0]).
+__device__ __forceinline__ void scale_products(uint32_t (&pk)[8], uint32_t e, const uint16_t* __restrict__ gexp,
+                                               const uint16_t* __restrict__ glog) {
+#pragma unroll
+  for (int b = 0; b < 16; b += 2) {
+    uint32_t s0 = glog[1u << b] + e, s1 = glog[1u << (b + 1)] + e;
+    s0 = (s0 + (s0 >> 16)) & kMod16;
+    s1 = (s1 + (s1 >> 16)) & kMod16;
+    pk[b >> 1] = (uint32_t)gexp[s0] | ((uint32_t)gexp[s1] << 16);
+  }
+}
+
+template <int LGN, bool IFFT, bool SUB>
+__device__ __forceinline__ void layer(uint32_t* planes, const uint32_t* __restrict__ tw, uint32_t t, uint32_t ld) {
+  constexpr uint32_t n = 1u << LGN;
+  const uint32_t D = 1u << ld;
+  const uint32_t base = (t >> ld) << (ld + 1), a = base + (t & (D - 1));
+  uint32_t x[16], y[16], pk[8];
+  load_tw(pk, tw, base + D - 1);
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    x[j] = planes[j * n + a];
+    y[j] = planes[j * n + a + D];
+  }
+  if (IFFT) {
+#pragma unroll
+    for (int j = 0; j < 16; j++) y[j] ^= x[j];
+    mul_acc<SUB>(x, y, pk);
+  } else {
+    mul_acc<SUB>(x, y, pk);
+#pragma unroll
+    for (int j = 0; j < 16; j++) y[j] ^= x[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    planes[j * n + a] = x[j];
+    planes[j * n + a + D] = y[j];
+  }
+  __syncthreads();
+}
+
+// IFFT: layers 0 .. LGN-1; FFT: LGN-1 .. 0. Twiddles of layer ld at offset 0 over n = 2^LGN
+// points have Cantor representation below 2^(LGN - ld) (block base >> layer), i.e. they lie
+// in GF(2^8) once LGN - ld <= 8 (upload_tables checks every twiddle).
+template <int LGN, bool IFFT>
+__device__ __forceinline__ void transform(uint32_t* planes, const uint32_t* __restrict__ tw, uint32_t t) {
+#pragma unroll 1
+  for (uint32_t i = 0; i < (uint32_t)LGN; i++) {
+    const uint32_t ld = IFFT ? i : LGN - 1 - i;
+    if (LGN - ld <= 8)
+      layer<LGN, IFFT, true>(planes, tw, t, ld);
+    else
+      layer<LGN, IFFT, false>(planes, tw, t, ld);
+  }
+}
+
+// LDS: planes [16][n] | err [n] | point products [8][n] (PT) | present [n] bytes.
+template <int LGN>
+constexpr bool point_table() {
+  return LGN <= 10;
+}
+
+template <int LGN>
+constexpr size_t decode_gf16_lds() {
+  constexpr size_t n = size_t(1) << LGN;
+  return n * 64 + n * 4 + (point_table<LGN>() ? n * 32 : 0) + n;
+}
+
+// grid: x = axis, y = chunk set (chunks blockIdx.y, blockIdx.y + gridDim.y, ...).
+// shards: [naxes][n][len] in rsmt2d order (data then parity); present: [naxes][n].
+template <int LGN>
+__global__ __launch_bounds__(1 << (LGN - 1)) void k_rs_decode_gf16(uint8_t* __restrict__ shards,
+                                                                    const uint8_t* __restrict__ present, uint32_t len,
+                                                                    const uint16_t* __restrict__ gexp,
+                                                                    const uint16_t* __restrict__ glog,
+                                                                    const uint32_t* __restrict__ tw) {
+  constexpr uint32_t n = 1u << LGN, m = n / 2, NT = n / 2;
+  constexpr bool PT = point_table<LGN>();
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  uint32_t* planes = lds;
+  uint32_t* err = planes + 16 * n;
+  uint32_t* ppt = err + n;
+  uint8_t* pres = reinterpret_cast<uint8_t*>(ppt + (PT ? 8 * n : 0));
+  uint32_t* tl = planes;  // error-locator scratch, before the first chunk
+  const uint32_t t = threadIdx.x;
+  uint8_t* axis = shards + (uint64_t)blockIdx.x * n * len;
+  const uint8_t* pa = present + (uint64_t)blockIdx.x * n;
+  // point p in Leopard order: p < m -> parity shard p (rsmt2d index m + p); else data p - m
+  for (uint32_t p = t; p < n; p += NT) pres[p] = pa[p < m ? m + p : p - m] ? 1 : 0;
+  __syncthreads();
+  // err[i] = sum_{e erased} log0[i ^ e] mod 65535: FWHT of the erasure indicator and of
+  // log0, pointwise product, FWHT back, times 1/n = 2^(16 - LGN) (as k_rs_decode)
+  for (uint32_t i = t; i < n; i += NT) {
+    err[i] = pres[i] ? 0u : 1u;
+    tl[i] = i == 0 ? 0u : (uint32_t)glog[i];
+  }
+  __syncthreads();
+  auto fwht = [&](uint32_t* v0, uint32_t* v1) {
+#pragma unroll 1
+    for (uint32_t lh = 0; lh < (uint32_t)LGN; lh++) {
+      const uint32_t h = 1u << lh;
+      const uint32_t a = ((t >> lh) << (lh + 1)) | (t & (h - 1)), b = a + h;
+      uint32_t x = v0[a], y = v0[b];
+      v0[a] = (x + y >= kMod16) ? x + y - kMod16 : x + y;
+      v0[b] = (x >= y) ? x - y : x + kMod16 - y;
+      if (v1) {
+        x = v1[a];
+        y = v1[b];
+        v1[a] = (x + y >= kMod16) ? x + y - kMod16 : x + y;
+        v1[b] = (x >= y) ? x - y : x + kMod16 - y;
+      }
+      __syncthreads();
+    }
+  };
+  fwht(err, tl);
+  for (uint32_t i = t; i < n; i += NT) err[i] = (err[i] * tl[i]) % kMod16;
+  __syncthreads();
+  fwht(err, nullptr);
+  constexpr uint32_t inv_n = (1u << (16 - LGN)) % kMod16;
+  for (uint32_t i = t; i < n; i += NT) {
+    const uint32_t e = (err[i] * inv_n) % kMod16;
+    // present points are scaled by exp(err), erased ones unscaled by exp(-err)
+    const uint32_t se = pres[i] ? e : (kMod16 - e) % kMod16;
+    if constexpr (PT) {
+      uint32_t pk[8];
+      scale_products(pk, se, gexp, glog);
+#pragma unroll
+      for (int q = 0; q < 8; q++) ppt[q * n + i] = pk[q];
+    } else {
+      err[i] = se;
+    }
+  }
+  auto point_products = [&](uint32_t (&pk)[8], uint32_t p) {
+    if constexpr (PT) {
+#pragma unroll
+      for (int q = 0; q < 8; q++) pk[q] = ppt[q * n + p];
+    } else {
+      scale_products(pk, err[p], gexp, glog);
+    }
+  };
+  for (uint32_t chunk = blockIdx.y; chunk < len / 64u; chunk += gridDim.y) {
+    const uint32_t coff = chunk * 64u;
+    __syncthreads();  // the previous chunk's stores (and the setup) are done with the LDS
+#pragma unroll
+    for (uint32_t h = 0; h < 2; h++) {
+      const uint32_t p = t + h * NT;
+      uint32_t out[16];
+#pragma unroll
+      for (int j = 0; j < 16; j++) out[j] = 0;
+      // erased points enter the transform as zero, whatever bytes the buffer holds there
+      if (pres[p]) {
+        const uint4* src = reinterpret_cast<const uint4*>(axis + (uint64_t)(p < m ? m + p : p - m) * len + coff);
+        uint32_t w[16], pk[8];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const uint4 v = src[q];
+          w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+        }
+        bs::tr8<0>(w);
+        bs::tr8<8>(w);
+        point_products(pk, p);
+        mul_acc<false>(out, w, pk);
+      }
+#pragma unroll
+      for (int j = 0; j < 16; j++) planes[j * n + p] = out[j];
+    }
+    __syncthreads();
+    transform<LGN, true>(planes, tw, t);
+    {  // formal derivative: new[x] = old[x] ^ xor_{s: bit s of x clear, x + 2^s < n} old[x + 2^s]
+      constexpr uint32_t R = 16 * n / NT;  // 32 items per thread
+      uint32_t acc[R];
+#pragma unroll
+      for (uint32_t r = 0; r < R; r++) {
+        const uint32_t it = t + r * NT, x = it & (n - 1), u = it >> LGN;
+        acc[r] = 0;
+#pragma unroll
+        for (uint32_t s = 1; s < n; s <<= 1)
+          if ((x & s) == 0) acc[r] ^= planes[u * n + x + s];
+      }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t r = 0; r < R; r++) planes[t + r * NT] ^= acc[r];
+      __syncthreads();
+    }
+    transform<LGN, false>(planes, tw, t);
+#pragma unroll
+    for (uint32_t h = 0; h < 2; h++) {
+      const uint32_t p = t + h * NT;
+      if (pres[p]) continue;
+      uint32_t w[16], pk[8], out[16];
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        w[j] = planes[j * n + p];
+        out[j] = 0;
+      }
+      point_products(pk, p);
+      mul_acc<false>(out, w, pk);
+      bs::tr8<0>(out);
+      bs::tr8<8>(out);
+      uint4* dst = reinterpret_cast<uint4*>(axis + (uint64_t)(p < m ? m + p : p - m) * len + coff);
+#pragma unroll
+      for (int q = 0; q < 4; q++) dst[q] = uint4{out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]};
+    }
+  }
+}
+
+}  // namespace
+
+bool rs_decode_gf16_supported(uint32_t n) { return n == 512 || n == 1024 || n == 2048; }
+
+hipError_t launch_rs_decode_gf16(uint8_t* shards, const uint8_t* present, uint32_t naxes, uint32_t n, uint32_t len,
+                                 const DeviceTables& t, hipStream_t s) {
+  if (!naxes) return hipSuccess;
+  if (!rs_decode_gf16_supported(n) || len == 0 || len % 64 || !t.tw16) return hipErrorInvalidValue;
+  const uint32_t nch = len / 64;
+  // enough workgroups to fill the chip; each one computes its axis's error locator once
+  // for all the chunks it takes
+  uint32_t sets = (512 + naxes - 1) / naxes;
+  sets = sets < 1 ? 1 : (sets > nch ? nch : sets);
+  const dim3 grid(naxes, sets);
+  auto go = [&](auto kern, size_t lds) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, grid, dim3(n / 2), lds, s, shards, present, len, t.exp16, t.log16, t.tw16);
+  };
+  switch (n) {
+    case 512: go(k_rs_decode_gf16<9>, decode_gf16_lds<9>()); break;
+    case 1024: go(k_rs_decode_gf16<10>, decode_gf16_lds<10>()); break;
+    default: go(k_rs_decode_gf16<11>, decode_gf16_lds<11>()); break;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace cel

@@ -65,7 +65,23 @@ hipError_t upload_tables(DeviceTables* t) {
     for (uint32_t n = 0; n < 4; n++) one[4] |= (n << 6) << (8 * n);
     for (int i = 0; i < 8; i++) mul8[255 * 8 + i] = one[i];
   }
+  // GF(2^16) decoder twiddles: basis products P_b = c * (1 << b) of c = exp(skew[s]) for
+  // s < 2047 (n <= 2048 points), two per dword; the zero-twiddle sentinel gives zeros
+  std::vector<uint32_t> tw16(2047 * 8, 0);
+  for (uint32_t i = 0; i < 2047; i++)
+    for (uint32_t b = 0; b < 16; b++)
+      if (f16.skew[i] != f16.mod) tw16[i * 8 + b / 2] |= f16.mul_log(1u << b, f16.skew[i]) << (16 * (b & 1));
+  // the decoder treats layer ld of an n = 2^lgn transform as a GF(2^8) product when
+  // lgn - ld <= 8: every such twiddle must have Cantor representation < 256
+  for (uint32_t lgn = 9; lgn <= 11; lgn++)
+    for (uint32_t ld = lgn >= 8 ? lgn - 8 : 0; ld < lgn; ld++)
+      for (uint32_t base = 0; base < (1u << lgn); base += 2u << ld) {
+        const uint32_t sk = f16.skew[base + (1u << ld) - 1];
+        if (sk != f16.mod && f16.exp[sk] >= 256) return hipErrorInvalidValue;
+      }
   hipError_t e;
+  if ((e = hipMalloc(&t->tw16, tw16.size() * 4)) != hipSuccess) return e;
+  if ((e = hipMemcpy(t->tw16, tw16.data(), tw16.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return e;
   if ((e = hipMalloc(&t->tw8, tw.size() * 4)) != hipSuccess) return e;
   if ((e = hipMalloc(&t->mul8, mul8.size() * 4)) != hipSuccess) return e;
   if ((e = hipMalloc(&t->exp16, 65536 * 2)) != hipSuccess) return e;
@@ -84,6 +100,7 @@ void free_tables(DeviceTables* t) {
   (void)hipFree(t->exp16);
   (void)hipFree(t->log16);
   (void)hipFree(t->skew16);
+  (void)hipFree(t->tw16);
   *t = DeviceTables{};
 }
 
@@ -652,6 +669,7 @@ hipError_t launch_rs_decode(uint8_t* shards, const uint8_t* present, uint32_t na
                        t.mul8);
   };
   if (rs_decode_axis_supported(n, len)) return launch_rs_decode_axis(shards, present, naxes, n, len, t.mul8, s);
+  if (rs_decode_gf16_supported(n)) return launch_rs_decode_gf16(shards, present, naxes, n, len, t, s);
   switch (n) {  // GF(2^8): the point count is a template constant (unrolled layers)
     case 2: go(k_rs_decode<false, 2>); break;
     case 4: go(k_rs_decode<false, 4>); break;
