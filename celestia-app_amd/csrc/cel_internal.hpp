@@ -50,8 +50,14 @@ struct DeviceTables {
   uint16_t* log16 = nullptr;   // [65536]
   uint16_t* skew16 = nullptr;  // [65535]
   uint32_t* mul8 = nullptr;    // [256][8] GF(2^8) product tables indexed by log value (decoder)
-  uint32_t* tw16 = nullptr;    // [2047][8] GF(2^16) basis products c*(1 << i) of twiddle skew[s] (decoder)
+  uint32_t* tw16 = nullptr;    // [2047][8] GF(2^16) decoder twiddles: products c*b_i in tower coordinates
+  uint16_t* tower16 = nullptr; // [256 + 256 + 16] Cantor -> tower coordinates (lo, hi byte), b_i (decoder)
 };
+
+// Block size 2^J of the GF(2^16) decoder's products by twiddles below 2^r (Cantor
+// representation): such a twiddle lies in GF(2^(2^J)), the smallest Cantor subfield holding
+// span(beta_0 .. beta_{r-1}).
+constexpr uint32_t decode16_level(uint32_t r) { return r <= 1 ? 0 : r <= 2 ? 1 : r <= 4 ? 2 : r <= 8 ? 3 : 4; }
 
 // roctx range over a phase's launches (rocprofv3 --marker-trace shows them on the host
 // timeline; the launches themselves are asynchronous, so a range brackets their enqueue).

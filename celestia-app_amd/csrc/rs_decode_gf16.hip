@@ -10,10 +10,20 @@
 // in dwords 8-15. An 8x8 bit transpose in each byte lane (bs::tr8) turns each half into 8
 // bit planes: plane i (i < 8 from the lo half, 8 + (i - 8) from the hi half) holds bit i
 // of the 32 symbols' Cantor representations. Multiplying by a constant c is GF(2)-linear:
-// plane j of c*y is the xor of the planes i of y whose basis product P_i = c*(1 << i) has
-// bit j set, 16x16 masked xors (one v_bfe + one v_bitop3 each). The basis products of
-// every twiddle come from a 64 KiB table built on the host (DeviceTables::tw16); those of
-// the per-point scales (exp(+-err)) from the exp/log tables, once per workgroup.
+// plane j of c*y is the xor of the planes i of y whose basis product P_i = c*b_i has
+// coordinate j set, masked xors of one v_bfe + one v_bitop3 each (one v_bitop3 and an
+// s_bfe where the twiddle is wave-uniform).
+//
+// Tower basis. Inside the transform the planes hold coordinates in the basis b_i = prod of
+// gamma_k = beta_{2^k} over the set bits k of i (beta: the Cantor basis). The twiddles of a
+// layer with block bases below 2^r lie in the subfield GF(2^(2^J)), J = decode16_level(r),
+// and a product by such an element maps every block of 2^J consecutive coordinates onto
+// itself: 16 * 2^J masked xors instead of 256 (n = 1024: 256, 256, 128 x 4, 64, 64, 32, 16
+// over the ten layers). The change of basis rides on the per-point scales, which are
+// general products anyway: present points are scaled from Cantor planes into tower
+// planes, erased ones unscaled from tower planes back to Cantor planes. Twiddle products
+// come from a 64 KiB table built on the host (DeviceTables::tw16), the scales' from the
+// exp/log tables, once per workgroup.
 //
 // The previous LDS decoder looked every symbol's log and exp up in the 128 KiB global
 // tables (two gathers per product): k=512 repair's 1024-axis row pass took 16.2 ms,
@@ -34,16 +44,15 @@ namespace {
 
 constexpr uint32_t kMod16 = 65535u;
 
-// x ^= c*y (32 symbols, bit planes); pk[i / 2] half i % 2 holds P_i = c * (1 << i).
-// SUB: c lies in the subfield GF(2^8) (Cantor representation < 256), so P_i < 256 for
-// i < 8 and those rows never reach the hi planes.
-template <bool SUB>
+// x ^= c*y (32 symbols, bit planes); pk[i / 2] half i % 2 holds P_i = c * b_i. J: c lies
+// in GF(2^(2^J)), so P_i only reaches the coordinates of its own block of 2^J.
+template <int J>
 __device__ __forceinline__ void mul_acc(uint32_t (&x)[16], const uint32_t (&y)[16], const uint32_t (&pk)[8]) {
 #pragma unroll
   for (int i = 0; i < 16; i++) {
 #pragma unroll
     for (int j = 0; j < 16; j++) {
-      if (SUB && i < 8 && j >= 8) continue;
+      if ((i >> J) != (j >> J)) continue;
       const uint32_t msk = (uint32_t)__builtin_amdgcn_sbfe((int)pk[i >> 1], 16 * (i & 1) + j, 1);
       x[j] = __builtin_amdgcn_bitop3_b32(x[j], msk, y[i], 0x78);  // x ^ (msk & y)
     }
@@ -57,26 +66,45 @@ __device__ __forceinline__ void load_tw(uint32_t (&pk)[8], const uint32_t* __res
   pk[4] = b.x; pk[5] = b.y; pk[6] = b.z; pk[7] = b.w;
 }
 
-// Basis products of exp(e): P_b = exp[log[1 << b] + e] (e < 65535; a partial reduction
-// may give 65535, and exp[65535] = exp[0]).
-__device__ __forceinline__ void scale_products(uint32_t (&pk)[8], uint32_t e, const uint16_t* __restrict__ gexp,
-                                               const uint16_t* __restrict__ glog) {
+// Per-point products. Scale (present points, Cantor planes in, tower planes out):
+// P_i = T(exp(e) * (1 << i)); unscale (erased points, tower in, Cantor out):
+// P_i = exp(e) * b_i. exp(e) * a = exp[log a + e] (e < 65535; a partial reduction may give
+// 65535, and exp[65535] = exp[0]). tower: T by lo and hi byte, then b_i (DeviceTables).
+__device__ __forceinline__ uint32_t exp_mul(uint32_t la, uint32_t e, const uint16_t* __restrict__ gexp) {
+  uint32_t s = la + e;
+  s = (s + (s >> 16)) & kMod16;
+  return gexp[s];
+}
+
+__device__ __forceinline__ void scale_products(uint32_t (&pk)[8], uint32_t e, bool in, const uint16_t* __restrict__ gexp,
+                                               const uint16_t* __restrict__ glog, const uint16_t* __restrict__ tower) {
 #pragma unroll
   for (int b = 0; b < 16; b += 2) {
-    uint32_t s0 = glog[1u << b] + e, s1 = glog[1u << (b + 1)] + e;
-    s0 = (s0 + (s0 >> 16)) & kMod16;
-    s1 = (s1 + (s1 >> 16)) & kMod16;
-    pk[b >> 1] = (uint32_t)gexp[s0] | ((uint32_t)gexp[s1] << 16);
+    uint32_t p[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      if (in) {
+        const uint32_t c = exp_mul(glog[1u << (b + h)], e, gexp);
+        p[h] = (uint32_t)tower[c & 255] ^ (uint32_t)tower[256 + (c >> 8)];
+      } else {
+        p[h] = exp_mul(glog[tower[512 + b + h]], e, gexp);
+      }
+    }
+    pk[b >> 1] = p[0] | (p[1] << 16);
   }
 }
 
-template <int LGN, bool IFFT, bool SUB>
+// One radix-2 layer, one butterfly per thread. UNI: D >= 64, so the 64 lanes of a wave share
+// the block base and the twiddle (its masks go to SGPRs).
+template <int LGN, bool IFFT, int J, bool UNI>
 __device__ __forceinline__ void layer(uint32_t* planes, const uint32_t* __restrict__ tw, uint32_t t, uint32_t ld) {
   constexpr uint32_t n = 1u << LGN;
   const uint32_t D = 1u << ld;
   const uint32_t base = (t >> ld) << (ld + 1), a = base + (t & (D - 1));
   uint32_t x[16], y[16], pk[8];
-  load_tw(pk, tw, base + D - 1);
+  uint32_t sk = base + D - 1;
+  if (UNI) sk = __builtin_amdgcn_readfirstlane(sk);
+  load_tw(pk, tw, sk);
 #pragma unroll
   for (int j = 0; j < 16; j++) {
     x[j] = planes[j * n + a];
@@ -85,9 +113,9 @@ __device__ __forceinline__ void layer(uint32_t* planes, const uint32_t* __restri
   if (IFFT) {
 #pragma unroll
     for (int j = 0; j < 16; j++) y[j] ^= x[j];
-    mul_acc<SUB>(x, y, pk);
+    mul_acc<J>(x, y, pk);
   } else {
-    mul_acc<SUB>(x, y, pk);
+    mul_acc<J>(x, y, pk);
 #pragma unroll
     for (int j = 0; j < 16; j++) y[j] ^= x[j];
   }
@@ -100,24 +128,41 @@ __device__ __forceinline__ void layer(uint32_t* planes, const uint32_t* __restri
 }
 
 // IFFT: layers 0 .. LGN-1; FFT: LGN-1 .. 0. Twiddles of layer ld at offset 0 over n = 2^LGN
-// points have Cantor representation below 2^(LGN - ld) (block base >> layer), i.e. they lie
-// in GF(2^8) once LGN - ld <= 8 (upload_tables checks every twiddle).
+// points have Cantor representation below 2^(LGN - ld) (block base >> layer), so they lie in
+// GF(2^(2^J)) with J = decode16_level(LGN - ld) (upload_tables checks every twiddle).
 template <int LGN, bool IFFT>
 __device__ __forceinline__ void transform(uint32_t* planes, const uint32_t* __restrict__ tw, uint32_t t) {
 #pragma unroll 1
   for (uint32_t i = 0; i < (uint32_t)LGN; i++) {
     const uint32_t ld = IFFT ? i : LGN - 1 - i;
-    if (LGN - ld <= 8)
-      layer<LGN, IFFT, true>(planes, tw, t, ld);
-    else
-      layer<LGN, IFFT, false>(planes, tw, t, ld);
+    const uint32_t J = decode16_level(LGN - ld);
+    if (ld >= 6) {  // LGN <= 11: J <= 3
+      switch (J) {
+        case 0: layer<LGN, IFFT, 0, true>(planes, tw, t, ld); break;
+        case 1: layer<LGN, IFFT, 1, true>(planes, tw, t, ld); break;
+        case 2: layer<LGN, IFFT, 2, true>(planes, tw, t, ld); break;
+        default: layer<LGN, IFFT, 3, true>(planes, tw, t, ld); break;
+      }
+    } else {  // LGN >= 9: J >= 2
+      switch (J) {
+        case 2: layer<LGN, IFFT, 2, false>(planes, tw, t, ld); break;
+        case 3: layer<LGN, IFFT, 3, false>(planes, tw, t, ld); break;
+        default: layer<LGN, IFFT, 4, false>(planes, tw, t, ld); break;
+      }
+    }
   }
 }
 
-// LDS: planes [16][n] | err [n] | point products [8][n] (PT) | present [n] bytes.
+// LDS: planes [16][n] | err [n] | point products [8][n] (n <= 1024) | present [n] bytes.
+// CEL_D16_PT (A/B knob): 1 keeps the per-point products in LDS for n <= 1024 (computed
+// once per workgroup); 0 recomputes them per chunk from the exp/log tables, for a smaller
+// LDS footprint (n = 1024: 69 KiB, two workgroups per CU, instead of 101 KiB).
+#ifndef CEL_D16_PT
+#define CEL_D16_PT 1
+#endif
 template <int LGN>
 constexpr bool point_table() {
-  return LGN <= 10;
+  return CEL_D16_PT && LGN <= 10;
 }
 
 template <int LGN>
@@ -133,7 +178,8 @@ __global__ __launch_bounds__(1 << (LGN - 1)) void k_rs_decode_gf16(uint8_t* __re
                                                                     const uint8_t* __restrict__ present, uint32_t len,
                                                                     const uint16_t* __restrict__ gexp,
                                                                     const uint16_t* __restrict__ glog,
-                                                                    const uint32_t* __restrict__ tw) {
+                                                                    const uint32_t* __restrict__ tw,
+                                                                    const uint16_t* __restrict__ tower) {
   constexpr uint32_t n = 1u << LGN, m = n / 2, NT = n / 2;
   constexpr bool PT = point_table<LGN>();
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -183,7 +229,7 @@ __global__ __launch_bounds__(1 << (LGN - 1)) void k_rs_decode_gf16(uint8_t* __re
     const uint32_t se = pres[i] ? e : (kMod16 - e) % kMod16;
     if constexpr (PT) {
       uint32_t pk[8];
-      scale_products(pk, se, gexp, glog);
+      scale_products(pk, se, pres[i], gexp, glog, tower);
 #pragma unroll
       for (int q = 0; q < 8; q++) ppt[q * n + i] = pk[q];
     } else {
@@ -195,7 +241,7 @@ __global__ __launch_bounds__(1 << (LGN - 1)) void k_rs_decode_gf16(uint8_t* __re
 #pragma unroll
       for (int q = 0; q < 8; q++) pk[q] = ppt[q * n + p];
     } else {
-      scale_products(pk, err[p], gexp, glog);
+      scale_products(pk, err[p], pres[p], gexp, glog, tower);
     }
   };
   for (uint32_t chunk = blockIdx.y; chunk < len / 64u; chunk += gridDim.y) {
@@ -219,7 +265,7 @@ __global__ __launch_bounds__(1 << (LGN - 1)) void k_rs_decode_gf16(uint8_t* __re
         bs::tr8<0>(w);
         bs::tr8<8>(w);
         point_products(pk, p);
-        mul_acc<false>(out, w, pk);
+        mul_acc<4>(out, w, pk);
       }
 #pragma unroll
       for (int j = 0; j < 16; j++) planes[j * n + p] = out[j];
@@ -254,7 +300,7 @@ __global__ __launch_bounds__(1 << (LGN - 1)) void k_rs_decode_gf16(uint8_t* __re
         out[j] = 0;
       }
       point_products(pk, p);
-      mul_acc<false>(out, w, pk);
+      mul_acc<4>(out, w, pk);
       bs::tr8<0>(out);
       bs::tr8<8>(out);
       uint4* dst = reinterpret_cast<uint4*>(axis + (uint64_t)(p < m ? m + p : p - m) * len + coff);
@@ -271,7 +317,7 @@ bool rs_decode_gf16_supported(uint32_t n) { return n == 512 || n == 1024 || n ==
 hipError_t launch_rs_decode_gf16(uint8_t* shards, const uint8_t* present, uint32_t naxes, uint32_t n, uint32_t len,
                                  const DeviceTables& t, hipStream_t s) {
   if (!naxes) return hipSuccess;
-  if (!rs_decode_gf16_supported(n) || len == 0 || len % 64 || !t.tw16) return hipErrorInvalidValue;
+  if (!rs_decode_gf16_supported(n) || len == 0 || len % 64 || !t.tw16 || !t.tower16) return hipErrorInvalidValue;
   const uint32_t nch = len / 64;
   // enough workgroups to fill the chip; each one computes its axis's error locator once
   // for all the chunks it takes
@@ -280,7 +326,8 @@ hipError_t launch_rs_decode_gf16(uint8_t* shards, const uint8_t* present, uint32
   const dim3 grid(naxes, sets);
   auto go = [&](auto kern, size_t lds) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, grid, dim3(n / 2), lds, s, shards, present, len, t.exp16, t.log16, t.tw16);
+    hipLaunchKernelGGL(kern, grid, dim3(n / 2), lds, s, shards, present, len, t.exp16, t.log16, t.tw16,
+                       t.tower16);
   };
   switch (n) {
     case 512: go(k_rs_decode_gf16<9>, decode_gf16_lds<9>()); break;

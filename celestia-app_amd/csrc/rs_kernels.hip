@@ -65,23 +65,58 @@ hipError_t upload_tables(DeviceTables* t) {
     for (uint32_t n = 0; n < 4; n++) one[4] |= (n << 6) << (8 * n);
     for (int i = 0; i < 8; i++) mul8[255 * 8 + i] = one[i];
   }
-  // GF(2^16) decoder twiddles: basis products P_b = c * (1 << b) of c = exp(skew[s]) for
-  // s < 2047 (n <= 2048 points), two per dword; the zero-twiddle sentinel gives zeros
+  // GF(2^16) decoder (rs_decode_gf16.hip): products in the tower basis b_i = prod over the
+  // set bits k of i of gamma_k = beta_{2^k} (Cantor basis elements), in which a product by
+  // an element of the subfield GF(2^(2^J)) = span(beta_0 .. beta_{2^J - 1}) maps each
+  // block of 2^J consecutive coordinates onto itself. v[i]: Cantor representation of b_i;
+  // tinv: Cantor representation -> tower coordinates.
+  std::vector<uint16_t> v(16), tinv(65536), tower(512 + 16);
+  for (uint32_t i = 0; i < 16; i++) {
+    uint32_t x = 1;
+    for (uint32_t k = 0; k < 4; k++)
+      if (i >> k & 1) x = f16.mul(x, 1u << (1u << k));
+    v[i] = (uint16_t)x;
+  }
+  {
+    std::vector<uint8_t> seen(65536, 0);
+    for (uint32_t c = 0; c < 65536; c++) {
+      uint32_t r = 0;
+      for (uint32_t i = 0; i < 16; i++)
+        if (c >> i & 1) r ^= v[i];
+      if (seen[r]) return hipErrorInvalidValue;  // not a basis
+      seen[r] = 1;
+      tinv[r] = (uint16_t)c;
+    }
+  }
+  for (uint32_t u = 0; u < 256; u++) {
+    tower[u] = tinv[u];
+    tower[256 + u] = tinv[u << 8];
+  }
+  for (uint32_t i = 0; i < 16; i++) tower[512 + i] = v[i];
+  // twiddle skew[s] (s < 2047: n <= 2048 points): P_i = c * b_i in tower coordinates, two
+  // per dword; the zero-twiddle sentinel gives zeros
   std::vector<uint32_t> tw16(2047 * 8, 0);
   for (uint32_t i = 0; i < 2047; i++)
     for (uint32_t b = 0; b < 16; b++)
-      if (f16.skew[i] != f16.mod) tw16[i * 8 + b / 2] |= f16.mul_log(1u << b, f16.skew[i]) << (16 * (b & 1));
-  // the decoder treats layer ld of an n = 2^lgn transform as a GF(2^8) product when
-  // lgn - ld <= 8: every such twiddle must have Cantor representation < 256
+      if (f16.skew[i] != f16.mod) tw16[i * 8 + b / 2] |= (uint32_t)tinv[f16.mul_log(v[b], f16.skew[i])] << (16 * (b & 1));
+  // the decoder runs layer ld of an n = 2^lgn transform with blocks of 2^J coordinates,
+  // J = decode16_level(lgn - ld): every such twiddle must keep its blocks
   for (uint32_t lgn = 9; lgn <= 11; lgn++)
-    for (uint32_t ld = lgn >= 8 ? lgn - 8 : 0; ld < lgn; ld++)
+    for (uint32_t ld = 0; ld < lgn; ld++) {
+      const uint32_t J = decode16_level(lgn - ld);
       for (uint32_t base = 0; base < (1u << lgn); base += 2u << ld) {
-        const uint32_t sk = f16.skew[base + (1u << ld) - 1];
-        if (sk != f16.mod && f16.exp[sk] >= 256) return hipErrorInvalidValue;
+        const uint32_t s = base + (1u << ld) - 1;
+        for (uint32_t b = 0; b < 16; b++) {
+          const uint32_t blk = ((1u << (1u << J)) - 1) << ((b >> J) << J);
+          if ((tw16[s * 8 + b / 2] >> (16 * (b & 1)) & 0xFFFF) & ~blk) return hipErrorInvalidValue;
+        }
       }
+    }
   hipError_t e;
   if ((e = hipMalloc(&t->tw16, tw16.size() * 4)) != hipSuccess) return e;
   if ((e = hipMemcpy(t->tw16, tw16.data(), tw16.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return e;
+  if ((e = hipMalloc(&t->tower16, tower.size() * 2)) != hipSuccess) return e;
+  if ((e = hipMemcpy(t->tower16, tower.data(), tower.size() * 2, hipMemcpyHostToDevice)) != hipSuccess) return e;
   if ((e = hipMalloc(&t->tw8, tw.size() * 4)) != hipSuccess) return e;
   if ((e = hipMalloc(&t->mul8, mul8.size() * 4)) != hipSuccess) return e;
   if ((e = hipMalloc(&t->exp16, 65536 * 2)) != hipSuccess) return e;
@@ -101,6 +136,7 @@ void free_tables(DeviceTables* t) {
   (void)hipFree(t->log16);
   (void)hipFree(t->skew16);
   (void)hipFree(t->tw16);
+  (void)hipFree(t->tower16);
   *t = DeviceTables{};
 }
 

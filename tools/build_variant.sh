@@ -8,7 +8,7 @@ name=$1; flags=$2
 bd=build_variants/$name
 mkdir -p $bd variants
 HIPCC=/opt/rocm/bin/hipcc
-srcs="api.cpp square.cpp proof.cpp inclusion.cpp inclusion_paths.cpp rs_kernels.hip rs_bitslice.hip rs_axis.hip rs_decode_axis.hip rs_gf16x.hip nmt_kernels.hip repair_kernels.hip"
+srcs="api.cpp square.cpp proof.cpp inclusion.cpp inclusion_paths.cpp rs_kernels.hip rs_bitslice.hip rs_axis.hip rs_decode_axis.hip rs_decode_gf16.hip rs_gf16x.hip nmt_kernels.hip repair_kernels.hip"
 objs=""
 for f in $srcs; do
   extra=""
