@@ -153,22 +153,14 @@ __device__ __forceinline__ void transform(uint32_t* planes, const uint32_t* __re
   }
 }
 
-// LDS: planes [16][n] | err [n] | point products [8][n] (n <= 1024) | present [n] bytes.
-// CEL_D16_PT (A/B knob): 1 keeps the per-point products in LDS for n <= 1024 (computed
-// once per workgroup); 0 recomputes them per chunk from the exp/log tables, for a smaller
-// LDS footprint (n = 1024: 69 KiB, two workgroups per CU, instead of 101 KiB).
-#ifndef CEL_D16_PT
-#define CEL_D16_PT 1
-#endif
-template <int LGN>
-constexpr bool point_table() {
-  return CEL_D16_PT && LGN <= 10;
-}
-
+// LDS: planes [16][n] | err [n] | present [n] bytes | point order [n] u16. 71 KiB at
+// n = 1024: two workgroups per CU. (Keeping the per-point products in LDS, computed once
+// per workgroup instead of once per chunk, takes 101 KiB and one workgroup per CU:
+// 17 % slower, profiles/r3_decode_gf16_ab.txt.)
 template <int LGN>
 constexpr size_t decode_gf16_lds() {
   constexpr size_t n = size_t(1) << LGN;
-  return n * 64 + n * 4 + (point_table<LGN>() ? n * 32 : 0) + n;
+  return n * 64 + n * 4 + n + n * 2;
 }
 
 // grid: x = axis, y = chunk set (chunks blockIdx.y, blockIdx.y + gridDim.y, ...).
@@ -181,19 +173,40 @@ __global__ __launch_bounds__(1 << (LGN - 1)) void k_rs_decode_gf16(uint8_t* __re
                                                                     const uint32_t* __restrict__ tw,
                                                                     const uint16_t* __restrict__ tower) {
   constexpr uint32_t n = 1u << LGN, m = n / 2, NT = n / 2;
-  constexpr bool PT = point_table<LGN>();
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ uint32_t s_cnt[n / 64];
   uint32_t* planes = lds;
   uint32_t* err = planes + 16 * n;
-  uint32_t* ppt = err + n;
-  uint8_t* pres = reinterpret_cast<uint8_t*>(ppt + (PT ? 8 * n : 0));
+  uint8_t* pres = reinterpret_cast<uint8_t*>(err + n);
+  uint16_t* order = reinterpret_cast<uint16_t*>(pres + n);  // present points, then erased ones
   uint32_t* tl = planes;  // error-locator scratch, before the first chunk
-  const uint32_t t = threadIdx.x;
+  const uint32_t t = threadIdx.x, lane = t & 63;
   uint8_t* axis = shards + (uint64_t)blockIdx.x * n * len;
   const uint8_t* pa = present + (uint64_t)blockIdx.x * n;
   // point p in Leopard order: p < m -> parity shard p (rsmt2d index m + p); else data p - m
-  for (uint32_t p = t; p < n; p += NT) pres[p] = pa[p < m ? m + p : p - m] ? 1 : 0;
+  uint64_t bal[2];
+#pragma unroll
+  for (uint32_t h = 0; h < 2; h++) {
+    const uint32_t p = t + h * NT;
+    const bool pr = pa[p < m ? m + p : p - m] != 0;
+    pres[p] = pr ? 1 : 0;
+    bal[h] = __ballot(pr);
+    if (lane == 0) s_cnt[p >> 6] = (uint32_t)__popcll(bal[h]);
+  }
   __syncthreads();
+  // the present points in ascending order, then the erased ones: the scale and unscale
+  // passes take one point per thread with divergence only at the boundary
+  uint32_t np = 0;
+#pragma unroll 1
+  for (uint32_t g = 0; g < n / 64; g++) np += s_cnt[g];
+#pragma unroll
+  for (uint32_t h = 0; h < 2; h++) {
+    const uint32_t p = t + h * NT;
+    uint32_t before = (uint32_t)__popcll(bal[h] & ((1ull << lane) - 1));
+#pragma unroll 1
+    for (uint32_t g = 0; g < (p >> 6); g++) before += s_cnt[g];
+    order[pres[p] ? before : np + p - before] = (uint16_t)p;
+  }
   // err[i] = sum_{e erased} log0[i ^ e] mod 65535: FWHT of the erasure indicator and of
   // log0, pointwise product, FWHT back, times 1/n = 2^(16 - LGN) (as k_rs_decode)
   for (uint32_t i = t; i < n; i += NT) {
@@ -226,35 +239,19 @@ __global__ __launch_bounds__(1 << (LGN - 1)) void k_rs_decode_gf16(uint8_t* __re
   for (uint32_t i = t; i < n; i += NT) {
     const uint32_t e = (err[i] * inv_n) % kMod16;
     // present points are scaled by exp(err), erased ones unscaled by exp(-err)
-    const uint32_t se = pres[i] ? e : (kMod16 - e) % kMod16;
-    if constexpr (PT) {
-      uint32_t pk[8];
-      scale_products(pk, se, pres[i], gexp, glog, tower);
-#pragma unroll
-      for (int q = 0; q < 8; q++) ppt[q * n + i] = pk[q];
-    } else {
-      err[i] = se;
-    }
+    err[i] = pres[i] ? e : (kMod16 - e) % kMod16;
   }
-  auto point_products = [&](uint32_t (&pk)[8], uint32_t p) {
-    if constexpr (PT) {
-#pragma unroll
-      for (int q = 0; q < 8; q++) pk[q] = ppt[q * n + p];
-    } else {
-      scale_products(pk, err[p], pres[p], gexp, glog, tower);
-    }
-  };
   for (uint32_t chunk = blockIdx.y; chunk < len / 64u; chunk += gridDim.y) {
     const uint32_t coff = chunk * 64u;
     __syncthreads();  // the previous chunk's stores (and the setup) are done with the LDS
 #pragma unroll
     for (uint32_t h = 0; h < 2; h++) {
-      const uint32_t p = t + h * NT;
+      const uint32_t idx = t + h * NT, p = order[idx];
       uint32_t out[16];
 #pragma unroll
       for (int j = 0; j < 16; j++) out[j] = 0;
       // erased points enter the transform as zero, whatever bytes the buffer holds there
-      if (pres[p]) {
+      if (idx < np) {
         const uint4* src = reinterpret_cast<const uint4*>(axis + (uint64_t)(p < m ? m + p : p - m) * len + coff);
         uint32_t w[16], pk[8];
 #pragma unroll
@@ -264,7 +261,7 @@ __global__ __launch_bounds__(1 << (LGN - 1)) void k_rs_decode_gf16(uint8_t* __re
         }
         bs::tr8<0>(w);
         bs::tr8<8>(w);
-        point_products(pk, p);
+        scale_products(pk, err[p], true, gexp, glog, tower);
         mul_acc<4>(out, w, pk);
       }
 #pragma unroll
@@ -290,16 +287,17 @@ __global__ __launch_bounds__(1 << (LGN - 1)) void k_rs_decode_gf16(uint8_t* __re
     }
     transform<LGN, false>(planes, tw, t);
 #pragma unroll
-    for (uint32_t h = 0; h < 2; h++) {
-      const uint32_t p = t + h * NT;
-      if (pres[p]) continue;
+    for (uint32_t h = 0; h < 2; h++) {  // (h = 1 only when fewer than half are present)
+      const uint32_t idx = np + t + h * NT;
+      if (idx >= n) continue;
+      const uint32_t p = order[idx];
       uint32_t w[16], pk[8], out[16];
 #pragma unroll
       for (int j = 0; j < 16; j++) {
         w[j] = planes[j * n + p];
         out[j] = 0;
       }
-      point_products(pk, p);
+      scale_products(pk, err[p], false, gexp, glog, tower);
       mul_acc<4>(out, w, pk);
       bs::tr8<0>(out);
       bs::tr8<8>(out);
