@@ -925,6 +925,8 @@ static cel_status fuzz(cel_ctx* ctx, hipStream_t s) {
 
 // Re-encode check of na gathered axes at `dense` on stream s: the data half of each axis
 // is encoded again and compared with its parity half; mismatches set flags[is_col*W + axis].
+// k = 256, 512: one launch of the GF(2^16) register kernel in check mode; else encode into
+// b.tmp and k_cmp.
 static cel_status encode_check(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_col, uint32_t na, const uint8_t* dense,
                                const int32_t* idx, hipStream_t s) {
   const uint32_t W = 2 * k;
@@ -942,6 +944,15 @@ static cel_status encode_check(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_c
   g.axes = na;
   g.nsq = 1;
   hipError_t e;
+  if (k == 256 || k == 512) {  // GF(2^16): the register kernel compares with the parity half as it goes
+    g.out = const_cast<uint8_t*>(dense) + (uint64_t)k * kShare;
+    g.out_sq = g.in_sq;
+    g.out_axis = g.in_axis;
+    g.chk_flags = b.flags + (size_t)is_col * W;
+    g.chk_idx = idx;
+    if ((e = launch_rs_encode(g, ctx->tables, s)) != hipSuccess) return hip_fail(ctx, e, "encoding check");
+    return CEL_OK;
+  }
   if ((e = launch_rs_encode(g, ctx->tables, s)) != hipSuccess) return hip_fail(ctx, e, "re-encode");
   if ((e = launch_cmp(b.tmp, (uint64_t)k * kShare, dense + (uint64_t)k * kShare, (uint64_t)W * kShare,
                       (uint64_t)k * kShare, na, b.flags + (size_t)is_col * W, s, idx)) != hipSuccess)

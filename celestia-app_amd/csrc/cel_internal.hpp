@@ -42,6 +42,11 @@ struct RsGeom {
   uint32_t len;   // bytes per shard (multiple of 64)
   uint32_t axes;  // axes per square
   uint32_t nsq;   // squares
+  // Check mode (GF(2^16) register kernel, n = 256/512, nsq == 1): nothing is stored; the
+  // computed parity is compared with the bytes at `out` and a mismatch in axis a sets
+  // chk_flags[chk_idx ? chk_idx[a] : a]. nullptr = encode.
+  int32_t* chk_flags;
+  const int32_t* chk_idx;
 };
 
 struct DeviceTables {

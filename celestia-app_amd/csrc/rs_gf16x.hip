@@ -351,7 +351,7 @@ __device__ __forceinline__ void pair_lo_hi(uint32_t (&w)[NW]) {
 // Tile = (square z, axis x, 64-byte column cb): one wave. Shard j of the axis sits at
 // in + z*in_sq + x*in_axis + place(j) + 64*cb (see RsGeom; blocked placement for the
 // output and the data copy when blk_log != 0).
-template <int LOGK>
+template <int LOGK, bool CHECK = false>
 __global__ __launch_bounds__(256, LOGK == 9 ? 3 : 4) void k_rs_gf16x(RsGeom g) {
   constexpr int K = 1 << LOGK;
   constexpr int NR = K / 8;
@@ -434,10 +434,21 @@ __global__ __launch_bounds__(256, LOGK == 9 ? 3 : 4) void k_rs_gf16x(RsGeom g) {
   const auto rout = rsrc(g.out + (uint64_t)z * g.out_sq + (uint64_t)x * g.out_axis);
   const uint32_t out_shard = (uint32_t)g.out_shard, out_blk = (uint32_t)g.out_blk;
   const uint32_t vout = place(lane_bits, out_shard, out_blk) + col;
+  if constexpr (CHECK) {  // repair's encoding check: compare with the parity in place
+    uint32_t diff = 0;
 #pragma unroll
-  for (int i = 0; i < NR; i++) {
-    const uint32_t so = __builtin_amdgcn_readfirstlane(place(reg_bits((uint32_t)i), out_shard, out_blk));
-    __builtin_amdgcn_raw_buffer_store_b64(D2{w[2 * i], w[2 * i + 1]}, rout, vout, so, 0);
+    for (int i = 0; i < NR; i++) {
+      const uint32_t so = __builtin_amdgcn_readfirstlane(place(reg_bits((uint32_t)i), out_shard, out_blk));
+      const auto v = __builtin_amdgcn_raw_buffer_load_b64(rout, vout, so, 0);
+      diff |= (v[0] ^ w[2 * i]) | (v[1] ^ w[2 * i + 1]);
+    }
+    if (__any(diff != 0) && lane == 0) atomicOr(g.chk_flags + (g.chk_idx ? g.chk_idx[x] : (int32_t)x), 1);
+  } else {
+#pragma unroll
+    for (int i = 0; i < NR; i++) {
+      const uint32_t so = __builtin_amdgcn_readfirstlane(place(reg_bits((uint32_t)i), out_shard, out_blk));
+      __builtin_amdgcn_raw_buffer_store_b64(D2{w[2 * i], w[2 * i + 1]}, rout, vout, so, 0);
+    }
   }
 }
 
@@ -446,7 +457,12 @@ static hipError_t launch(const RsGeom& g, hipStream_t s) {
   const uint64_t tiles = (uint64_t)g.axes * (g.len / 64u) * g.nsq;
   if (tiles == 0) return hipSuccess;
   if (tiles > 0xFFFFFFF0ull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_rs_gf16x<LOGK>, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, s, g);
+  if (g.chk_flags) {
+    if (g.nsq != 1 || g.dcopy) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_rs_gf16x<LOGK, true>), dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, s, g);
+  } else {
+    hipLaunchKernelGGL((k_rs_gf16x<LOGK, false>), dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, s, g);
+  }
   return hipGetLastError();
 }
 

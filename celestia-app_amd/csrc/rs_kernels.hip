@@ -326,9 +326,13 @@ __global__ __launch_bounds__(256) void k_rs_encode_gf16(RsGeom g, const uint16_t
 hipError_t launch_rs_encode(const RsGeom& g, const DeviceTables& t, hipStream_t s) {
   if (g.axes == 0 || g.nsq == 0) return hipSuccess;
   if (g.blk_log && !((g.n == 256 || g.n == 512) && g.len % 512 == 0)) return hipErrorInvalidValue;
-  if (2 * g.n <= 256) return g.n <= 16 ? launch_rs_encode_bitslice(g, s) : launch_rs_encode_axis(g, s);
+  if (2 * g.n <= 256) {
+    if (g.chk_flags) return hipErrorInvalidValue;
+    return g.n <= 16 ? launch_rs_encode_bitslice(g, s) : launch_rs_encode_axis(g, s);
+  }
   if (g.n > kMaxGf16Width || g.len % 64 != 0) return hipErrorInvalidValue;
   if (g.n == 256 || g.n == 512) return launch_rs_encode_gf16x(g, s);
+  if (g.chk_flags) return hipErrorInvalidValue;  // check mode: the register kernel only
   dim3 grid(g.axes, g.len / 64, g.nsq);
   const size_t lds = (size_t)g.n * 64;
   if (lds > 64 * 1024)
