@@ -53,9 +53,8 @@ struct DeviceTables {
   uint32_t* tw8 = nullptr;     // [255][8] GF(2^8) twiddle product tables, indexed by skew index
   uint16_t* exp16 = nullptr;   // [65536]
   uint16_t* log16 = nullptr;   // [65536]
-  uint16_t* skew16 = nullptr;  // [65535]
   uint32_t* mul8 = nullptr;    // [256][8] GF(2^8) product tables indexed by log value (decoder)
-  uint32_t* tw16 = nullptr;    // [2047][8] GF(2^16) decoder twiddles: products c*b_i in tower coordinates
+  uint32_t* tw16 = nullptr;    // [4095][8] GF(2^16) bit-plane twiddles: products c*b_i in tower coordinates
   uint16_t* tower16 = nullptr; // [256 + 256 + 16] Cantor -> tower coordinates (lo, hi byte), b_i (decoder)
 };
 
@@ -170,6 +169,8 @@ hipError_t launch_commitment(const uint8_t* d_cells, uint32_t k, uint32_t r0, ui
 // [naxes][2n][len] buffer with a [naxes][2n] present mask. In place.
 // GF(2^16) erasure decode over n = 512, 1024 or 2048 points (rs_decode_gf16.hip).
 bool rs_decode_gf16_supported(uint32_t n);
+// GF(2^16) encode of 1024 or 2048 data shards in bit planes (codec API).
+hipError_t launch_rs_encode_gf16p(const RsGeom& g, const DeviceTables& t, hipStream_t s);
 hipError_t launch_rs_decode_gf16(uint8_t* shards, const uint8_t* present, uint32_t naxes, uint32_t n, uint32_t len,
                                  const DeviceTables& t, hipStream_t s);
 hipError_t launch_rs_decode(uint8_t* shards, const uint8_t* present, uint32_t naxes, uint32_t n,

@@ -96,19 +96,31 @@ __device__ __forceinline__ void scale_products(uint32_t (&pk)[8], uint32_t e, bo
 
 // One radix-2 layer, one butterfly per thread. UNI: D >= 64, so the 64 lanes of a wave share
 // the block base and the twiddle (its masks go to SGPRs).
+// LDS word of point p in a plane: p with its low 5 bits flipped when bit 5 is set. A
+// layer's x (or y) points seen by 32 lanes of a ds_read_b32 group differ in 5 of the bits
+// 0-5 of p, so they fall on 32 distinct banks ((word mod 32)) for every D: without the
+// flip D = 1..16 were 2-way conflicts.
+// (CEL_D16_SWZ=0: the plain layout, for A/B runs.)
+#ifndef CEL_D16_SWZ
+#define CEL_D16_SWZ 1
+#endif
+__device__ __forceinline__ uint32_t swz(uint32_t p) { return CEL_D16_SWZ ? p ^ ((0u - ((p >> 5) & 1u)) & 31u) : p; }
+
 template <int LGN, bool IFFT, int J, bool UNI>
-__device__ __forceinline__ void layer(uint32_t* planes, const uint32_t* __restrict__ tw, uint32_t t, uint32_t ld) {
+__device__ __forceinline__ void layer(uint32_t* planes, const uint32_t* __restrict__ tw, uint32_t t, uint32_t ld,
+                                      uint32_t off) {
   constexpr uint32_t n = 1u << LGN;
   const uint32_t D = 1u << ld;
   const uint32_t base = (t >> ld) << (ld + 1), a = base + (t & (D - 1));
+  const uint32_t sa = swz(a), sb = swz(a + D);
   uint32_t x[16], y[16], pk[8];
-  uint32_t sk = base + D - 1;
+  uint32_t sk = off + base + D - 1;
   if (UNI) sk = __builtin_amdgcn_readfirstlane(sk);
   load_tw(pk, tw, sk);
 #pragma unroll
   for (int j = 0; j < 16; j++) {
-    x[j] = planes[j * n + a];
-    y[j] = planes[j * n + a + D];
+    x[j] = planes[j * n + sa];
+    y[j] = planes[j * n + sb];
   }
   if (IFFT) {
 #pragma unroll
@@ -121,33 +133,37 @@ __device__ __forceinline__ void layer(uint32_t* planes, const uint32_t* __restri
   }
 #pragma unroll
   for (int j = 0; j < 16; j++) {
-    planes[j * n + a] = x[j];
-    planes[j * n + a + D] = y[j];
+    planes[j * n + sa] = x[j];
+    planes[j * n + sb] = y[j];
   }
   __syncthreads();
 }
 
-// IFFT: layers 0 .. LGN-1; FFT: LGN-1 .. 0. Twiddles of layer ld at offset 0 over n = 2^LGN
-// points have Cantor representation below 2^(LGN - ld) (block base >> layer), so they lie in
-// GF(2^(2^J)) with J = decode16_level(LGN - ld) (upload_tables checks every twiddle).
-template <int LGN, bool IFFT>
-__device__ __forceinline__ void transform(uint32_t* planes, const uint32_t* __restrict__ tw, uint32_t t) {
+// IFFT: layers 0 .. LGN-1; FFT: LGN-1 .. 0, over n = 2^LGN points at offset `off` (a
+// multiple of n). The twiddle of layer ld has Cantor representation (off + block base) >> ld,
+// below 2^(RB - ld) with RB = log2(off + n), so it lies in GF(2^(2^J)) with J =
+// decode16_level(RB - ld) (upload_tables checks every twiddle the kernels use). The decoder
+// runs both at offset 0 (RB = LGN); the encoder's IFFT runs at offset n (RB = LGN + 1).
+template <int LGN, bool IFFT, int RB = LGN>
+__device__ __forceinline__ void transform(uint32_t* planes, const uint32_t* __restrict__ tw, uint32_t t,
+                                          uint32_t off = 0) {
+  static_assert(RB >= 9 && RB <= 12, "levels: J >= 2 below layer 6, J <= 3 from it");
 #pragma unroll 1
   for (uint32_t i = 0; i < (uint32_t)LGN; i++) {
     const uint32_t ld = IFFT ? i : LGN - 1 - i;
-    const uint32_t J = decode16_level(LGN - ld);
-    if (ld >= 6) {  // LGN <= 11: J <= 3
+    const uint32_t J = decode16_level(RB - ld);
+    if (ld >= 6) {  // D >= 64: wave-uniform twiddle
       switch (J) {
-        case 0: layer<LGN, IFFT, 0, true>(planes, tw, t, ld); break;
-        case 1: layer<LGN, IFFT, 1, true>(planes, tw, t, ld); break;
-        case 2: layer<LGN, IFFT, 2, true>(planes, tw, t, ld); break;
-        default: layer<LGN, IFFT, 3, true>(planes, tw, t, ld); break;
+        case 0: layer<LGN, IFFT, 0, true>(planes, tw, t, ld, off); break;
+        case 1: layer<LGN, IFFT, 1, true>(planes, tw, t, ld, off); break;
+        case 2: layer<LGN, IFFT, 2, true>(planes, tw, t, ld, off); break;
+        default: layer<LGN, IFFT, 3, true>(planes, tw, t, ld, off); break;
       }
-    } else {  // LGN >= 9: J >= 2
+    } else {
       switch (J) {
-        case 2: layer<LGN, IFFT, 2, false>(planes, tw, t, ld); break;
-        case 3: layer<LGN, IFFT, 3, false>(planes, tw, t, ld); break;
-        default: layer<LGN, IFFT, 4, false>(planes, tw, t, ld); break;
+        case 2: layer<LGN, IFFT, 2, false>(planes, tw, t, ld, off); break;
+        case 3: layer<LGN, IFFT, 3, false>(planes, tw, t, ld, off); break;
+        default: layer<LGN, IFFT, 4, false>(planes, tw, t, ld, off); break;
       }
     }
   }
@@ -265,24 +281,34 @@ __global__ __launch_bounds__(1 << (LGN - 1)) void k_rs_decode_gf16(uint8_t* __re
         mul_acc<4>(out, w, pk);
       }
 #pragma unroll
-      for (int j = 0; j < 16; j++) planes[j * n + p] = out[j];
+      for (int j = 0; j < 16; j++) planes[j * n + swz(p)] = out[j];
     }
     __syncthreads();
     transform<LGN, true>(planes, tw, t);
     {  // formal derivative: new[x] = old[x] ^ xor_{s: bit s of x clear, x + 2^s < n} old[x + 2^s]
-      constexpr uint32_t R = 16 * n / NT;  // 32 items per thread
-      uint32_t acc[R];
+      // (a thread takes points t and t + n/2 in all 16 planes: one address per (point, s))
+      uint32_t acc[2][16];
 #pragma unroll
-      for (uint32_t r = 0; r < R; r++) {
-        const uint32_t it = t + r * NT, x = it & (n - 1), u = it >> LGN;
-        acc[r] = 0;
+      for (uint32_t h = 0; h < 2; h++) {
+        const uint32_t x = t + h * NT;
 #pragma unroll
-        for (uint32_t s = 1; s < n; s <<= 1)
-          if ((x & s) == 0) acc[r] ^= planes[u * n + x + s];
+        for (int u = 0; u < 16; u++) acc[h][u] = 0;
+#pragma unroll
+        for (uint32_t s = 1; s < n; s <<= 1) {
+          if ((x & s) == 0) {
+            const uint32_t a = swz(x + s);
+#pragma unroll
+            for (int u = 0; u < 16; u++) acc[h][u] ^= planes[u * n + a];
+          }
+        }
       }
       __syncthreads();
 #pragma unroll
-      for (uint32_t r = 0; r < R; r++) planes[t + r * NT] ^= acc[r];
+      for (uint32_t h = 0; h < 2; h++) {
+        const uint32_t a = swz(t + h * NT);
+#pragma unroll
+        for (int u = 0; u < 16; u++) planes[u * n + a] ^= acc[h][u];
+      }
       __syncthreads();
     }
     transform<LGN, false>(planes, tw, t);
@@ -294,7 +320,7 @@ __global__ __launch_bounds__(1 << (LGN - 1)) void k_rs_decode_gf16(uint8_t* __re
       uint32_t w[16], pk[8], out[16];
 #pragma unroll
       for (int j = 0; j < 16; j++) {
-        w[j] = planes[j * n + p];
+        w[j] = planes[j * n + swz(p)];
         out[j] = 0;
       }
       scale_products(pk, err[p], false, gexp, glog, tower);
@@ -304,6 +330,79 @@ __global__ __launch_bounds__(1 << (LGN - 1)) void k_rs_decode_gf16(uint8_t* __re
       uint4* dst = reinterpret_cast<uint4*>(axis + (uint64_t)(p < m ? m + p : p - m) * len + coff);
 #pragma unroll
       for (int q = 0; q < 4; q++) dst[q] = uint4{out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]};
+    }
+  }
+}
+
+// Encoder for 1024 and 2048 data shards (the codec API; squares stop at k = 512, which
+// the register kernel rs_gf16x.hip takes): the data shards are scaled by 1 into tower
+// planes, IFFT over the m points at offset m, FFT at offset 0, back to Cantor planes.
+// grid: x = axis, y = chunk set, z = square; m / 2 threads; LDS: m 64-byte chunks.
+template <int LGM>
+__global__ __launch_bounds__(1 << (LGM - 1)) void k_rs_encode_gf16p(RsGeom g, const uint16_t* __restrict__ gexp,
+                                                                     const uint16_t* __restrict__ glog,
+                                                                     const uint32_t* __restrict__ tw,
+                                                                     const uint16_t* __restrict__ tower) {
+  constexpr uint32_t m = 1u << LGM, NT = m / 2;
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  uint32_t* planes = lds;
+  const uint32_t t = threadIdx.x;
+  const uint8_t* in = g.in + (uint64_t)blockIdx.z * g.in_sq + (uint64_t)blockIdx.x * g.in_axis;
+  uint8_t* out = g.out + (uint64_t)blockIdx.z * g.out_sq + (uint64_t)blockIdx.x * g.out_axis;
+  uint32_t to_tower[8], to_cantor[8];  // the change of basis as products by 1
+  scale_products(to_tower, 0, true, gexp, glog, tower);
+  scale_products(to_cantor, 0, false, gexp, glog, tower);
+  for (uint32_t chunk = blockIdx.y; chunk < g.len / 64u; chunk += gridDim.y) {
+    const uint32_t coff = chunk * 64u;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t h = 0; h < 2; h++) {
+      const uint32_t p = t + h * NT;
+      const uint4* src = reinterpret_cast<const uint4*>(in + (uint64_t)p * g.in_shard + coff);
+      uint32_t w[16], o[16];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint4 v = src[q];
+        w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+      }
+      bs::tr8<0>(w);
+      bs::tr8<8>(w);
+#pragma unroll
+      for (int j = 0; j < 16; j++) o[j] = 0;
+      uint32_t pk[8];
+#pragma unroll
+      for (int q = 0; q < 8; q++) {  // opaque per use: else all 256 masks are hoisted and held
+        pk[q] = __builtin_amdgcn_readfirstlane(to_tower[q]);
+        asm volatile("" : "+s"(pk[q]));
+      }
+      mul_acc<4>(o, w, pk);
+#pragma unroll
+      for (int j = 0; j < 16; j++) planes[j * m + swz(p)] = o[j];
+    }
+    __syncthreads();
+    transform<LGM, true, LGM + 1>(planes, tw, t, m);
+    transform<LGM, false>(planes, tw, t);
+#pragma unroll
+    for (uint32_t h = 0; h < 2; h++) {
+      const uint32_t p = t + h * NT;
+      uint32_t w[16], o[16];
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        w[j] = planes[j * m + swz(p)];
+        o[j] = 0;
+      }
+      uint32_t pk[8];
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        pk[q] = __builtin_amdgcn_readfirstlane(to_cantor[q]);
+        asm volatile("" : "+s"(pk[q]));
+      }
+      mul_acc<4>(o, w, pk);
+      bs::tr8<0>(o);
+      bs::tr8<8>(o);
+      uint4* dst = reinterpret_cast<uint4*>(out + (uint64_t)p * g.out_shard + coff);
+#pragma unroll
+      for (int q = 0; q < 4; q++) dst[q] = uint4{o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]};
     }
   }
 }
@@ -332,6 +431,30 @@ hipError_t launch_rs_decode_gf16(uint8_t* shards, const uint8_t* present, uint32
     case 1024: go(k_rs_decode_gf16<10>, decode_gf16_lds<10>()); break;
     default: go(k_rs_decode_gf16<11>, decode_gf16_lds<11>()); break;
   }
+  return hipGetLastError();
+}
+
+}  // namespace cel
+
+namespace cel {
+
+hipError_t launch_rs_encode_gf16p(const RsGeom& g, const DeviceTables& t, hipStream_t s) {
+  if ((g.n != 1024 && g.n != 2048) || g.len == 0 || g.len % 64 || g.dcopy || g.blk_log || g.chk_flags || !t.tw16 ||
+      !t.tower16)
+    return hipErrorInvalidValue;
+  const uint32_t nch = g.len / 64;
+  const uint64_t tiles = (uint64_t)g.axes * g.nsq;
+  uint32_t sets = (uint32_t)((512 + tiles - 1) / tiles);
+  sets = sets < 1 ? 1 : (sets > nch ? nch : sets);
+  const dim3 grid(g.axes, sets, g.nsq);
+  auto go = [&](auto kern, size_t lds) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, grid, dim3(g.n / 2), lds, s, g, t.exp16, t.log16, t.tw16, t.tower16);
+  };
+  if (g.n == 1024)
+    go(k_rs_encode_gf16p<10>, (size_t)1024 * 64);
+  else
+    go(k_rs_encode_gf16p<11>, (size_t)2048 * 64);
   return hipGetLastError();
 }
 

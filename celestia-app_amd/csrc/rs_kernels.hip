@@ -93,25 +93,34 @@ hipError_t upload_tables(DeviceTables* t) {
     tower[256 + u] = tinv[u << 8];
   }
   for (uint32_t i = 0; i < 16; i++) tower[512 + i] = v[i];
-  // twiddle skew[s] (s < 2047: n <= 2048 points): P_i = c * b_i in tower coordinates, two
-  // per dword; the zero-twiddle sentinel gives zeros
-  std::vector<uint32_t> tw16(2047 * 8, 0);
-  for (uint32_t i = 0; i < 2047; i++)
+  // twiddle skew[s] (s < 4095: decoder n <= 2048 points at offset 0, encoder m <= 2048 at
+  // offset m): P_i = c * b_i in tower coordinates, two per dword; the zero-twiddle sentinel
+  // gives zeros
+  constexpr uint32_t kTw16 = 4095;
+  std::vector<uint32_t> tw16(kTw16 * 8, 0);
+  for (uint32_t i = 0; i < kTw16; i++)
     for (uint32_t b = 0; b < 16; b++)
       if (f16.skew[i] != f16.mod) tw16[i * 8 + b / 2] |= (uint32_t)tinv[f16.mul_log(v[b], f16.skew[i])] << (16 * (b & 1));
-  // the decoder runs layer ld of an n = 2^lgn transform with blocks of 2^J coordinates,
-  // J = decode16_level(lgn - ld): every such twiddle must keep its blocks
-  for (uint32_t lgn = 9; lgn <= 11; lgn++)
-    for (uint32_t ld = 0; ld < lgn; ld++) {
-      const uint32_t J = decode16_level(lgn - ld);
-      for (uint32_t base = 0; base < (1u << lgn); base += 2u << ld) {
-        const uint32_t s = base + (1u << ld) - 1;
+  // the kernels run layer ld of a 2^lgn-point transform at offset off with blocks of 2^J
+  // coordinates, J = decode16_level(log2(off + 2^lgn) - ld): every such twiddle must keep
+  // its blocks. (lgn, offset): decoder (9..11, 0); encoder IFFT (10..11, 2^lgn), FFT (10..11, 0).
+  struct Tr {
+    uint32_t lgn, off;
+  };
+  const Tr trs[] = {{9, 0}, {10, 0}, {11, 0}, {10, 1024}, {11, 2048}};
+  for (const Tr& tr : trs) {
+    const uint32_t rb = tr.off ? tr.lgn + 1 : tr.lgn;
+    for (uint32_t ld = 0; ld < tr.lgn; ld++) {
+      const uint32_t J = decode16_level(rb - ld);
+      for (uint32_t base = 0; base < (1u << tr.lgn); base += 2u << ld) {
+        const uint32_t s = tr.off + base + (1u << ld) - 1;
         for (uint32_t b = 0; b < 16; b++) {
           const uint32_t blk = ((1u << (1u << J)) - 1) << ((b >> J) << J);
           if ((tw16[s * 8 + b / 2] >> (16 * (b & 1)) & 0xFFFF) & ~blk) return hipErrorInvalidValue;
         }
       }
     }
+  }
   hipError_t e;
   if ((e = hipMalloc(&t->tw16, tw16.size() * 4)) != hipSuccess) return e;
   if ((e = hipMemcpy(t->tw16, tw16.data(), tw16.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return e;
@@ -121,12 +130,11 @@ hipError_t upload_tables(DeviceTables* t) {
   if ((e = hipMalloc(&t->mul8, mul8.size() * 4)) != hipSuccess) return e;
   if ((e = hipMalloc(&t->exp16, 65536 * 2)) != hipSuccess) return e;
   if ((e = hipMalloc(&t->log16, 65536 * 2)) != hipSuccess) return e;
-  if ((e = hipMalloc(&t->skew16, 65535 * 2)) != hipSuccess) return e;
   if ((e = hipMemcpy(t->tw8, tw.data(), tw.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return e;
   if ((e = hipMemcpy(t->mul8, mul8.data(), mul8.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return e;
   if ((e = hipMemcpy(t->exp16, f16.exp.data(), 65536 * 2, hipMemcpyHostToDevice)) != hipSuccess) return e;
   if ((e = hipMemcpy(t->log16, f16.log.data(), 65536 * 2, hipMemcpyHostToDevice)) != hipSuccess) return e;
-  return hipMemcpy(t->skew16, f16.skew.data(), 65535 * 2, hipMemcpyHostToDevice);
+  return hipSuccess;
 }
 
 void free_tables(DeviceTables* t) {
@@ -134,7 +142,6 @@ void free_tables(DeviceTables* t) {
   (void)hipFree(t->mul8);
   (void)hipFree(t->exp16);
   (void)hipFree(t->log16);
-  (void)hipFree(t->skew16);
   (void)hipFree(t->tw16);
   (void)hipFree(t->tower16);
   *t = DeviceTables{};
@@ -179,150 +186,12 @@ __device__ __forceinline__ uint32_t gf8_mul4(uint32_t y, const PermTab& t) {
                                      __builtin_amdgcn_perm(0u, t.t2, s2), 0x96);
 }
 
-// ------------------------------------------------- LDS transform kernels
-
-// Field ops for the LDS kernels. A "unit" is one dword of 4 GF(2^8) symbols, or
-// a GF(2^16) quad: lo-byte dword j and hi-byte dword j+8 of a 64-byte chunk.
-struct Gf8Ops {
-  static constexpr uint32_t MOD = 255;
-  static constexpr int UNITS = 16;  // dwords per 64-byte chunk
-  const uint8_t* lexp;
-  const uint8_t* llog;
-  __device__ uint32_t mul_log1(uint32_t a, uint32_t lm) const {
-    if (!a) return 0;
-    uint32_t s = llog[a] + lm;
-    s = (s + (s >> 8)) & 255u;
-    return lexp[s];
-  }
-  __device__ void muladd(uint32_t* chunk_x, const uint32_t* chunk_y, int u, uint32_t lm) const {
-    const uint32_t y = chunk_y[u];
-    uint32_t p = 0;
-#pragma unroll
-    for (int b = 0; b < 4; b++) p |= mul_log1((y >> (8 * b)) & 0xFF, lm) << (8 * b);
-    chunk_x[u] ^= p;
-  }
-  __device__ void xorin(uint32_t* chunk_y, const uint32_t* chunk_x, int u) const { chunk_y[u] ^= chunk_x[u]; }
-  __device__ void scale(uint32_t* chunk, int u, uint32_t lm) const {
-    uint32_t y = chunk[u], p = 0;
-#pragma unroll
-    for (int b = 0; b < 4; b++) p |= mul_log1((y >> (8 * b)) & 0xFF, lm) << (8 * b);
-    chunk[u] = p;
-  }
-};
-
-struct Gf16Ops {
-  static constexpr uint32_t MOD = 65535;
-  static constexpr int UNITS = 8;  // quads per 64-byte chunk
-  const uint16_t* __restrict__ gexp;
-  const uint16_t* __restrict__ glog;
-  __device__ uint32_t mul_log1(uint32_t a, uint32_t lm) const {
-    if (!a) return 0;
-    uint32_t s = glog[a] + lm;
-    s = (s + (s >> 16)) & 65535u;
-    return gexp[s];
-  }
-  __device__ void muladd(uint32_t* cx, const uint32_t* cy, int u, uint32_t lm) const {
-    const uint32_t lo = cy[u], hi = cy[u + 8];
-    uint32_t plo = 0, phi = 0;
-#pragma unroll
-    for (int b = 0; b < 4; b++) {
-      const uint32_t s = ((lo >> (8 * b)) & 0xFF) | (((hi >> (8 * b)) & 0xFF) << 8);
-      const uint32_t p = mul_log1(s, lm);
-      plo |= (p & 0xFF) << (8 * b);
-      phi |= (p >> 8) << (8 * b);
-    }
-    cx[u] ^= plo;
-    cx[u + 8] ^= phi;
-  }
-  __device__ void xorin(uint32_t* cy, const uint32_t* cx, int u) const {
-    cy[u] ^= cx[u];
-    cy[u + 8] ^= cx[u + 8];
-  }
-  __device__ void scale(uint32_t* c, int u, uint32_t lm) const {
-    const uint32_t lo = c[u], hi = c[u + 8];
-    uint32_t plo = 0, phi = 0;
-#pragma unroll
-    for (int b = 0; b < 4; b++) {
-      const uint32_t s = ((lo >> (8 * b)) & 0xFF) | (((hi >> (8 * b)) & 0xFF) << 8);
-      const uint32_t p = mul_log1(s, lm);
-      plo |= (p & 0xFF) << (8 * b);
-      phi |= (p >> 8) << (8 * b);
-    }
-    c[u] = plo;
-    c[u + 8] = phi;
-  }
-};
-
-// Radix-2 transform layers over `npts` chunks of 16 dwords in LDS.
-// ifft: D ascending, constant skew[off + base + D - 1]; y ^= x; x ^= y*c
-// fft:  D descending, constant skew[base + D - 1];      x ^= y*c; y ^= x
-template <class Ops, class SkewFn>
-__device__ void lds_ifft(const Ops& ops, uint32_t* lds, uint32_t npts, uint32_t off, SkewFn skew) {
-  const uint32_t items = (npts / 2) * Ops::UNITS;
-  for (uint32_t D = 1; D < npts; D <<= 1) {
-    for (uint32_t it = threadIdx.x; it < items; it += blockDim.x) {
-      const uint32_t pair = it / Ops::UNITS, u = it % Ops::UNITS;
-      const uint32_t base = (pair / D) * 2 * D, a = base + pair % D;
-      uint32_t* x = lds + a * 16;
-      uint32_t* y = lds + (a + D) * 16;
-      const uint32_t lm = skew(off + base + D - 1);
-      ops.xorin(y, x, u);
-      if (lm != Ops::MOD) ops.muladd(x, y, u, lm);
-    }
-    __syncthreads();
-  }
-}
-
-template <class Ops, class SkewFn>
-__device__ void lds_fft(const Ops& ops, uint32_t* lds, uint32_t npts, SkewFn skew) {
-  const uint32_t items = (npts / 2) * Ops::UNITS;
-  for (uint32_t D = npts >> 1; D >= 1; D >>= 1) {
-    for (uint32_t it = threadIdx.x; it < items; it += blockDim.x) {
-      const uint32_t pair = it / Ops::UNITS, u = it % Ops::UNITS;
-      const uint32_t base = (pair / D) * 2 * D, a = base + pair % D;
-      uint32_t* x = lds + a * 16;
-      uint32_t* y = lds + (a + D) * 16;
-      const uint32_t lm = skew(base + D - 1);
-      if (lm != Ops::MOD) ops.muladd(x, y, u, lm);
-      ops.xorin(y, x, u);
-    }
-    __syncthreads();
-  }
-}
-
-// GF(2^16) encode: grid x = axis, y = 64-byte chunk, z = square. LDS: n * 64 B.
-__global__ __launch_bounds__(256) void k_rs_encode_gf16(RsGeom g, const uint16_t* __restrict__ gexp,
-                                                        const uint16_t* __restrict__ glog,
-                                                        const uint16_t* __restrict__ gskew) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  const uint32_t n = g.n;
-  const uint32_t coff = blockIdx.y * 64u;
-  const uint8_t* src = g.in + (uint64_t)blockIdx.z * g.in_sq + (uint64_t)blockIdx.x * g.in_axis + coff;
-  uint8_t* dst = g.out + (uint64_t)blockIdx.z * g.out_sq + (uint64_t)blockIdx.x * g.out_axis + coff;
-  for (uint32_t it = threadIdx.x; it < n * 4; it += blockDim.x) {
-    const uint32_t i = it >> 2, q = it & 3;
-    const uint4 v = reinterpret_cast<const uint4*>(src + (uint64_t)i * g.in_shard)[q];
-    reinterpret_cast<uint4*>(lds)[it] = v;
-    if (g.dcopy)
-      reinterpret_cast<uint4*>(g.dcopy + (uint64_t)blockIdx.z * g.dc_sq + (uint64_t)blockIdx.x * g.dc_axis + coff +
-                               (uint64_t)i * g.dc_shard)[q] = v;
-  }
-  __syncthreads();
-  Gf16Ops ops{gexp, glog};
-  auto skew = [&](uint32_t i) { return (uint32_t)gskew[i]; };
-  lds_ifft(ops, lds, n, n, skew);
-  lds_fft(ops, lds, n, skew);
-  for (uint32_t it = threadIdx.x; it < n * 4; it += blockDim.x) {
-    const uint32_t i = it >> 2, q = it & 3;
-    reinterpret_cast<uint4*>(dst + (uint64_t)i * g.out_shard)[q] = reinterpret_cast<const uint4*>(lds)[it];
-  }
-}
-
 // GF(2^8) (2n <= 256): bit-sliced for n <= 16 (rs_bitslice.hip), one wave per axis slice
 // for n >= 32 (rs_axis.hip: k = 128, 32 squares, 15.2 us/square against 18.1 for the
 // workgroup-per-slice v_perm kernel this replaced, profiles/r1_axis_ab.txt).
 // GF(2^16): the constant-twiddle register kernel for n = 256, 512 (rs_gf16x.hip); the
-// LDS kernel for 1024 <= n <= kMaxGf16Width (codec API only: squares stop at k = 512).
+// bit-plane kernel for n = 1024, 2048 (rs_decode_gf16.hip; codec API only: squares stop at
+// k = 512).
 hipError_t launch_rs_encode(const RsGeom& g, const DeviceTables& t, hipStream_t s) {
   if (g.axes == 0 || g.nsq == 0) return hipSuccess;
   if (g.blk_log && !((g.n == 256 || g.n == 512) && g.len % 512 == 0)) return hipErrorInvalidValue;
@@ -333,12 +202,7 @@ hipError_t launch_rs_encode(const RsGeom& g, const DeviceTables& t, hipStream_t 
   if (g.n > kMaxGf16Width || g.len % 64 != 0) return hipErrorInvalidValue;
   if (g.n == 256 || g.n == 512) return launch_rs_encode_gf16x(g, s);
   if (g.chk_flags) return hipErrorInvalidValue;  // check mode: the register kernel only
-  dim3 grid(g.axes, g.len / 64, g.nsq);
-  const size_t lds = (size_t)g.n * 64;
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute((const void*)k_rs_encode_gf16, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(k_rs_encode_gf16, grid, dim3(256), lds, s, g, t.exp16, t.log16, t.skew16);
-  return hipGetLastError();
+  return launch_rs_encode_gf16p(g, t, s);  // n = 1024, 2048 (no data copy, linear placement)
 }
 
 // Row pass of the extension, Q0 rows -> Q1. Q0 is read from `ods` (and copied into the
@@ -410,54 +274,9 @@ hipError_t launch_extend(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t 
 //   erased i: shard_i = work[i] * exp(-err[i])
 // Erased parity shards are revealed by the same formula (the codeword is unique).
 
-template <class Ops, class SkewFn>
-__device__ void decode_chunk(const Ops& ops, uint32_t* lds, uint32_t* err, const uint8_t* pres, uint32_t m,
-                             SkewFn skew) {
-  const uint32_t n = 2 * m;
-  // work <- present * exp(err)
-  for (uint32_t it = threadIdx.x; it < n * Ops::UNITS; it += blockDim.x) {
-    const uint32_t i = it / Ops::UNITS, u = it % Ops::UNITS;
-    if (pres[i]) ops.scale(lds + i * 16, u, err[i]);
-  }
-  __syncthreads();
-  lds_ifft(ops, lds, n, 0, skew);
-  // formal derivative: new[x] = old[x] ^ xor_{t: bit t of x clear, x + 2^t < n} old[x + 2^t].
-  // Sources are never modified before being read in the sequential reference loop,
-  // so processing x in descending order of blocks is unnecessary: read old values
-  // for all targets first (per lane, a unit at a time), then write.
-  for (uint32_t base = 0; base < n * Ops::UNITS; base += blockDim.x) {
-    const uint32_t it = base + threadIdx.x;
-    uint32_t acc[2] = {0, 0};
-    const bool active = it < n * Ops::UNITS;
-    uint32_t x = 0, u = 0;
-    if (active) {
-      x = it / Ops::UNITS;
-      u = it % Ops::UNITS;
-      for (uint32_t t = 1; t < n; t <<= 1) {
-        if ((x & t) == 0 && x + t < n) {
-          acc[0] ^= lds[(x + t) * 16 + u];
-          if (Ops::UNITS == 8) acc[1] ^= lds[(x + t) * 16 + u + 8];
-        }
-      }
-    }
-    __syncthreads();
-    if (active) {
-      lds[x * 16 + u] ^= acc[0];
-      if (Ops::UNITS == 8) lds[x * 16 + u + 8] ^= acc[1];
-    }
-    __syncthreads();
-  }
-  lds_fft(ops, lds, n, skew);
-  for (uint32_t it = threadIdx.x; it < n * Ops::UNITS; it += blockDim.x) {
-    const uint32_t i = it / Ops::UNITS, u = it % Ops::UNITS;
-    if (!pres[i]) ops.scale(lds + i * 16, u, (Ops::MOD - err[i]) % Ops::MOD);
-  }
-  __syncthreads();
-}
-
 // GF(2^8) decode of one 64-byte chunk with v_perm product tables staged in LDS
-// (ltw: twiddle tables by skew index, lmul: tables by log value; 5 dwords each) in
-// place of the per-byte log/exp lookups of Gf8Ops: same transform as decode_chunk.
+// (ltw: twiddle tables by skew index, lmul: tables by log value; 5 dwords each): the
+// transform above.
 // Layers go two at a time (radix 4: a thread owns one dword of four points, half the
 // LDS round trips and barriers of radix 2); the formal derivative reads every source
 // before one barrier and writes after it.
@@ -589,47 +408,40 @@ __device__ void decode_chunk_gf8p(uint32_t* lds, const uint32_t* err, const uint
 
 // grid: x = axis, y = 64-byte chunk. shards: [naxes][2m][len] in rsmt2d order
 // (data then parity); present: [naxes][2m].
-template <bool GF16, uint32_t N8>
+// GF(2^8) axes the register decoder does not take (2m = 2..256 points; m < 16 or a chunk
+// tail). GF(2^16): rs_decode_gf16.hip.
+template <uint32_t N8>
 __global__ __launch_bounds__(256) void k_rs_decode(uint8_t* shards, const uint8_t* present, uint32_t m,
-                                                   uint32_t len, const uint16_t* __restrict__ gexp,
-                                                   const uint16_t* __restrict__ glog,
-                                                   const uint16_t* __restrict__ gskew,
-                                                   const uint32_t* __restrict__ tw8,
+                                                   uint32_t len, const uint32_t* __restrict__ tw8,
                                                    const uint32_t* __restrict__ mul8) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const uint32_t n = 2 * m;
   uint32_t* err = lds + n * 16;
   uint32_t* ltw = err + 2 * n;      // (err + n: n words of error-locator scratch)
   uint32_t* lmul = ltw + 256 * 8;   // GF(2^8): [255][8] twiddle tables, [256][8] by log value (16-B aligned)
-  uint8_t* pres = reinterpret_cast<uint8_t*>(GF16 ? ltw : lmul + 256 * 8);
-  if (!GF16) {
-    for (uint32_t i = threadIdx.x; i < 255 * 2; i += blockDim.x)
-      reinterpret_cast<uint4*>(ltw)[i] = reinterpret_cast<const uint4*>(tw8)[i];
-    for (uint32_t i = threadIdx.x; i < 256 * 2; i += blockDim.x)
-      reinterpret_cast<uint4*>(lmul)[i] = reinterpret_cast<const uint4*>(mul8)[i];
-  }
+  uint8_t* pres = reinterpret_cast<uint8_t*>(lmul + 256 * 8);
+  for (uint32_t i = threadIdx.x; i < 255 * 2; i += blockDim.x)
+    reinterpret_cast<uint4*>(ltw)[i] = reinterpret_cast<const uint4*>(tw8)[i];
+  for (uint32_t i = threadIdx.x; i < 256 * 2; i += blockDim.x)
+    reinterpret_cast<uint4*>(lmul)[i] = reinterpret_cast<const uint4*>(mul8)[i];
   __shared__ uint8_t s_log[256];
   uint8_t* axis = shards + (uint64_t)blockIdx.x * n * len;
   const uint8_t* pa = present + (uint64_t)blockIdx.x * n;
   // position p in Leopard order: p < m -> parity shard p (rsmt2d index m + p); else data p - m.
   for (uint32_t p = threadIdx.x; p < n; p += blockDim.x) pres[p] = pa[p < m ? m + p : p - m] ? 1 : 0;
-  if (!GF16) {
-    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
-      s_log[i] = c_gf8.log[i];
-    }
-  }
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) s_log[i] = c_gf8.log[i];
   __syncthreads();
   // Error locator err[i] = sum_{e erased} log0[i ^ e] (mod MOD), an XOR convolution of
   // the erasure indicator with log0: FWHT both, multiply pointwise, FWHT back and scale
   // by 1/n = 2^(bits - log2 n) (2^bits = 1 mod MOD) - Leopard's own FWHT route, O(n log n)
   // instead of the O(n^2) direct sum.
   {
-    constexpr uint32_t MOD = GF16 ? 65535u : 255u;
-    constexpr uint32_t BITS = GF16 ? 16u : 8u;
+    constexpr uint32_t MOD = 255u;
+    constexpr uint32_t BITS = 8u;
     uint32_t* tl = err + n;
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
       err[i] = pres[i] ? 0u : 1u;
-      tl[i] = i == 0 ? 0u : (GF16 ? (uint32_t)glog[i] : (uint32_t)s_log[i]);
+      tl[i] = i == 0 ? 0u : (uint32_t)s_log[i];
     }
     __syncthreads();
     const uint32_t lgn = 31u - __builtin_clz(n);
@@ -672,12 +484,7 @@ __global__ __launch_bounds__(256) void k_rs_decode(uint8_t* shards, const uint8_
           pres[p] ? reinterpret_cast<const uint4*>(axis + (uint64_t)r * len + coff)[q] : uint4{0, 0, 0, 0};
     }
     __syncthreads();
-    if (GF16) {
-      Gf16Ops ops{gexp, glog};
-      decode_chunk(ops, lds, err, pres, m, [&](uint32_t i) { return (uint32_t)gskew[i]; });
-    } else {
-      if constexpr (N8 != 0) decode_chunk_gf8p<N8>(lds, err, pres, ltw, lmul);
-    }
+    decode_chunk_gf8p<N8>(lds, err, pres, ltw, lmul);
     for (uint32_t it = threadIdx.x; it < n * 4; it += blockDim.x) {
       const uint32_t p = it >> 2, q = it & 3;
       if (pres[p]) continue;
@@ -692,11 +499,13 @@ size_t decode_workspace_size(uint32_t, uint32_t) { return 0; }
 hipError_t launch_rs_decode(uint8_t* shards, const uint8_t* present, uint32_t naxes, uint32_t m, uint32_t len,
                             const DeviceTables& t, void*, hipStream_t s) {
   if (!naxes) return hipSuccess;
+  const uint32_t n = 2 * m;
+  if (rs_decode_axis_supported(n, len)) return launch_rs_decode_axis(shards, present, naxes, n, len, t.mul8, s);
+  if (rs_decode_gf16_supported(n)) return launch_rs_decode_gf16(shards, present, naxes, n, len, t, s);
+  if (n > 256 || len == 0 || len % 64) return hipErrorInvalidValue;
   hipError_t e = ensure_gf8_const();
   if (e != hipSuccess) return e;
-  const uint32_t n = 2 * m;
-  const size_t lds = (size_t)n * 64 + (size_t)n * 8 + n + (2 * m <= 256 ? (256 + 256) * 8 * 4 : 0);
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  const size_t lds = (size_t)n * 64 + (size_t)n * 8 + n + (256 + 256) * 8 * 4;
   // 2 chunks per workgroup: the per-axis setup (error locator, table staging) is shared
   // by both 64-byte chunks (1 and 4 measured slower, profiles/r1j_repair_cpw_ab.txt)
   constexpr uint32_t cpw = 2;
@@ -705,21 +514,17 @@ hipError_t launch_rs_decode(uint8_t* shards, const uint8_t* present, uint32_t na
   auto go = [&](auto kern) {
     if (lds > 64 * 1024)
       (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, shards, present, m, len, t.exp16, t.log16, t.skew16, t.tw8,
-                       t.mul8);
+    hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, shards, present, m, len, t.tw8, t.mul8);
   };
-  if (rs_decode_axis_supported(n, len)) return launch_rs_decode_axis(shards, present, naxes, n, len, t.mul8, s);
-  if (rs_decode_gf16_supported(n)) return launch_rs_decode_gf16(shards, present, naxes, n, len, t, s);
-  switch (n) {  // GF(2^8): the point count is a template constant (unrolled layers)
-    case 2: go(k_rs_decode<false, 2>); break;
-    case 4: go(k_rs_decode<false, 4>); break;
-    case 8: go(k_rs_decode<false, 8>); break;
-    case 16: go(k_rs_decode<false, 16>); break;
-    case 32: go(k_rs_decode<false, 32>); break;
-    case 64: go(k_rs_decode<false, 64>); break;
-    case 128: go(k_rs_decode<false, 128>); break;
-    case 256: go(k_rs_decode<false, 256>); break;
-    default: go(k_rs_decode<true, 0>); break;
+  switch (n) {  // the point count is a template constant (unrolled layers)
+    case 2: go(k_rs_decode<2>); break;
+    case 4: go(k_rs_decode<4>); break;
+    case 8: go(k_rs_decode<8>); break;
+    case 16: go(k_rs_decode<16>); break;
+    case 32: go(k_rs_decode<32>); break;
+    case 64: go(k_rs_decode<64>); break;
+    case 128: go(k_rs_decode<128>); break;
+    default: go(k_rs_decode<256>); break;
   }
   return hipGetLastError();
 }

@@ -17,6 +17,9 @@ cat gpurun_out/${tag}_bench.json
 timeout -k 10 300 python -u bench.py --mode repair --steps 20 --warmup 3 \
   > gpurun_out/${tag}_bench_repair.json 2> gpurun_out/${tag}_bench_repair.err || exit $?
 cat gpurun_out/${tag}_bench_repair.json
+timeout -k 10 300 python -u bench.py --mode repair --k 512 --steps 8 --warmup 2 --cpu-seconds 4 \
+  > gpurun_out/${tag}_bench_repair512.json 2> gpurun_out/${tag}_bench_repair512.err || exit $?
+cat gpurun_out/${tag}_bench_repair512.json
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --marker-trace --stats -d gpurun_out/${tag}_prof -o b --output-format csv -- \
   python3 bench.py --steps 5 --warmup 2 --no-host-io --k512-batch 8 > gpurun_out/${tag}_bench_prof.json 2>/dev/null || exit $?
