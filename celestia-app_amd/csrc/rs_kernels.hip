@@ -17,9 +17,9 @@
 // 3+3+2 bits and looks each piece up with one v_perm_b32 in an 8/8/4-entry
 // product table held in SGPRs: 10-12 VALU ops per 4 bytes.
 //
-// GF(2^16) (k >= 256) and the decoder stage a 64-byte chunk of every shard of
-// an axis in LDS (k <= 2048 -> <= 128 KiB) and run radix-2 layers with a
-// barrier per layer.
+// GF(2^16) runs in rs_gf16x.hip (encode, 256/512 data shards) and rs_decode_gf16.hip
+// (decode; encode of 1024/2048 shards). The GF(2^8) LDS decoder below takes the axes the
+// register decoder (rs_decode_axis.hip) does not.
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
