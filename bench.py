@@ -321,7 +321,8 @@ def run_repair(a):
     before the step's clock starts. host: host buffers in and out (cel_repair), PCIe
     copies included. Single rank.
     roofline: the decoder alone (cel_dev_decode over the row pass's axes of the same
-    mask: k_rs_decode_axis, register-resident GF(2^8)), algorithmic bytes = every shard of
+    mask: k_rs_decode_axis, register-resident GF(2^8); k >= 256: k_rs_decode_gf16, bit planes
+    in LDS), algorithmic bytes = every shard of
     every decoded axis read once + every missing shard written once, against HBM; the
     decoder is VALU-bound (~15K VALU per wave, one wave per SIMD at 239 axes), so the
     fraction says how far from streaming."""
@@ -431,7 +432,9 @@ def run_repair(a):
                                   else "(EDS resident in HBM; the damaged-copy restore runs before each step's "
                                        "clock)"),
                    "k": k, "parallelism": "single"},
-        "roofline": {"bound": "hbm", "kernel": "k_rs_decode_axis (cel_dev_decode, the row pass's axes)",
+        "roofline": {"bound": "hbm",
+                     "kernel": ("k_rs_decode_axis" if k <= 128 else "k_rs_decode_gf16 (bit planes)")
+                     + " (cel_dev_decode, the row pass's axes)",
                      "achieved": dec_bytes / t_dec / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": dec_bytes / t_dec / 1e9 / HBM_PEAK_GBS, "traffic": None,
                      "avg_launch_us": t_dec * 1e6, "axes": len(rows),
