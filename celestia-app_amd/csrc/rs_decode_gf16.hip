@@ -1,4 +1,5 @@
-// Leopard GF(2^16) erasure decode (2m = 512, 1024, 2048 points) in bit planes.
+// Leopard GF(2^16) erasure decode (2m = 512, 1024, 2048 points) and the codec encoder of
+// 1024/2048 data shards, in bit planes.
 //
 // Replaces klauspost/reedsolomon v1.12.1 leopard.go Reconstruct (catid/leopard's
 // ReedSolomonDecode) as rsmt2d v0.14.0 LeoRSCodec.Decode drives it above 256 shards
@@ -22,8 +23,9 @@
 // over the ten layers). The change of basis rides on the per-point scales, which are
 // general products anyway: present points are scaled from Cantor planes into tower
 // planes, erased ones unscaled from tower planes back to Cantor planes. Twiddle products
-// come from a 64 KiB table built on the host (DeviceTables::tw16), the scales' from the
-// exp/log tables, once per workgroup.
+// come from a 128 KiB table built on the host (DeviceTables::tw16), the scales' from the
+// exp/log tables, once per chunk. tests/test_gf16_planes.py checks both statements against
+// the field on the CPU.
 //
 // The previous LDS decoder looked every symbol's log and exp up in the 128 KiB global
 // tables (two gathers per product): k=512 repair's 1024-axis row pass took 16.2 ms,
@@ -31,7 +33,7 @@
 //
 // Layout: one workgroup per (axis, chunk set), n/2 threads (one butterfly each per layer),
 // the chunk's 16 planes of every point in LDS plane-major (plane j of point p at
-// [j * n + p]: consecutive lanes read consecutive words).
+// [j * n + swz(p)]: consecutive lanes read consecutive words).
 #include <hip/hip_runtime.h>
 
 #include "bitslice8.hpp"
