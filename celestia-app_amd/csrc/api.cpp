@@ -961,8 +961,8 @@ static cel_status encode_check(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_c
 }
 
 // Encoding check of na complete axes of the square (list idx on the device) on stream s:
-// one in-place launch (k_rs_check_axes) for k = 32..128, else gather into dchk and
-// encode_check.
+// one in-place launch for k = 32..128 (k_rs_check_axes) and k = 256/512 (k_rs_gf16x in
+// check mode), else gather into dchk and encode_check.
 static cel_status check_in_square(cel_ctx* ctx, RepairBufs& b, uint32_t k, int is_col, uint32_t na,
                                   const int32_t* idx, hipStream_t s) {
   const uint32_t W = 2 * k;
@@ -970,6 +970,24 @@ static cel_status check_in_square(cel_ctx* ctx, RepairBufs& b, uint32_t k, int i
   if (k >= 32 && k <= kMaxGf8Width) {
     if ((e = launch_rs_check_axes(b.eds, k, idx, is_col, na, b.flags + (size_t)is_col * W, s)) != hipSuccess)
       return hip_fail(ctx, e, "encoding check");
+    return CEL_OK;
+  }
+  if (k == 256 || k == 512) {  // the GF(2^16) register kernel in check mode, in place
+    const uint64_t row = (uint64_t)W * kShare;
+    RsGeom g{};
+    g.in = b.eds;
+    g.out = b.eds + (is_col ? (uint64_t)k * row : (uint64_t)k * kShare);
+    g.in_axis = g.out_axis = is_col ? kShare : row;
+    g.in_shard = g.out_shard = is_col ? row : kShare;
+    g.in_sq = g.out_sq = row * W;
+    g.n = k;
+    g.len = kShare;
+    g.axes = na;
+    g.nsq = 1;
+    g.chk_flags = b.flags + (size_t)is_col * W;
+    g.chk_idx = idx;
+    g.chk_axes = idx;
+    if ((e = launch_rs_encode(g, ctx->tables, s)) != hipSuccess) return hip_fail(ctx, e, "encoding check");
     return CEL_OK;
   }
   if ((e = launch_gather_axes(b.eds, b.mask, W, idx, is_col, na, b.dchk, b.dmask_chk, s)) != hipSuccess)

@@ -47,6 +47,10 @@ struct RsGeom {
   // chk_flags[chk_idx ? chk_idx[a] : a]. nullptr = encode.
   int32_t* chk_flags;
   const int32_t* chk_idx;
+  // Check mode only: axis a of the launch is axis chk_axes[a] of the square (in/out bases
+  // in + chk_axes[a]*in_axis, out + chk_axes[a]*out_axis), so the check reads the square in
+  // place. nullptr = axis a.
+  const int32_t* chk_axes;
 };
 
 struct DeviceTables {

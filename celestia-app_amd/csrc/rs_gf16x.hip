@@ -362,6 +362,7 @@ __global__ __launch_bounds__(256, LOGK == 9 ? 3 : 4) void k_rs_gf16x(RsGeom g) {
   if (tile >= (uint32_t)g.axes * nblk * g.nsq) return;
   const uint32_t cb = tile % nblk, r = tile / nblk;
   const uint32_t x = r % g.axes, z = r / g.axes;
+  const uint32_t xa = CHECK && g.chk_axes ? (uint32_t)g.chk_axes[x] : x;  // the axis addressed
   const uint32_t L = lane >> 3;
   const uint32_t col = cb * 64u + (lane & 7u) * 8u;  // 8 lanes x 8 B = one 64-byte block
   const uint32_t m7 = sconst<0x07070707u>(), m3 = sconst<0x03030303u>();
@@ -384,7 +385,7 @@ __global__ __launch_bounds__(256, LOGK == 9 ? 3 : 4) void k_rs_gf16x(RsGeom g) {
   const uint32_t lane_bits = L << 5;
   uint32_t w[NW];
   {
-    const auto rin = rsrc(g.in + (uint64_t)z * g.in_sq + (uint64_t)x * g.in_axis);
+    const auto rin = rsrc(g.in + (uint64_t)z * g.in_sq + (uint64_t)xa * g.in_axis);
     const uint32_t in_shard = (uint32_t)g.in_shard;
     const uint32_t vin = lane_bits * in_shard + col;
 #pragma unroll
@@ -431,7 +432,7 @@ __global__ __launch_bounds__(256, LOGK == 9 ? 3 : 4) void k_rs_gf16x(RsGeom g) {
   layer_a<LOGK, 0, false>(w, lane_tab<5>(mk0, mk1, mk2), m7, m3);
   convert(w, m7, m3);  // -> (lo, hi)
   pair_lo_hi(w);
-  const auto rout = rsrc(g.out + (uint64_t)z * g.out_sq + (uint64_t)x * g.out_axis);
+  const auto rout = rsrc(g.out + (uint64_t)z * g.out_sq + (uint64_t)xa * g.out_axis);
   const uint32_t out_shard = (uint32_t)g.out_shard, out_blk = (uint32_t)g.out_blk;
   const uint32_t vout = place(lane_bits, out_shard, out_blk) + col;
   if constexpr (CHECK) {  // repair's encoding check: compare with the parity in place
