@@ -175,6 +175,11 @@ __device__ __forceinline__ void transform(uint32_t* planes, const uint32_t* __re
 // n = 1024: two workgroups per CU. (Keeping the per-point products in LDS, computed once
 // per workgroup instead of once per chunk, takes 101 KiB and one workgroup per CU:
 // 17 % slower, profiles/r3_decode_gf16_ab.txt.)
+// CEL_D16_PREG (A/B knob): keep the per-point products of a thread's first present and
+// first erased point in registers across its chunks instead of recomputing them per chunk.
+#ifndef CEL_D16_PREG
+#define CEL_D16_PREG 0
+#endif
 template <int LGN>
 constexpr size_t decode_gf16_lds() {
   constexpr size_t n = size_t(1) << LGN;
@@ -259,6 +264,14 @@ __global__ __launch_bounds__(1 << (LGN - 1)) void k_rs_decode_gf16(uint8_t* __re
     // present points are scaled by exp(err), erased ones unscaled by exp(-err)
     err[i] = pres[i] ? e : (kMod16 - e) % kMod16;
   }
+#if CEL_D16_PREG
+  // the first present and the first erased point of this thread keep their products in
+  // registers across the chunks (the others, if any, look theirs up per chunk)
+  __syncthreads();
+  uint32_t pre0[8], post0[8];
+  if (t < np) scale_products(pre0, err[order[t]], true, gexp, glog, tower);
+  if (np + t < n) scale_products(post0, err[order[np + t]], false, gexp, glog, tower);
+#endif
   for (uint32_t chunk = blockIdx.y; chunk < len / 64u; chunk += gridDim.y) {
     const uint32_t coff = chunk * 64u;
     __syncthreads();  // the previous chunk's stores (and the setup) are done with the LDS
@@ -279,7 +292,19 @@ __global__ __launch_bounds__(1 << (LGN - 1)) void k_rs_decode_gf16(uint8_t* __re
         }
         bs::tr8<0>(w);
         bs::tr8<8>(w);
+#if CEL_D16_PREG
+        if (h == 0) {
+#pragma unroll
+          for (int q = 0; q < 8; q++) {  // opaque: else the masks are hoisted out of the loop
+            pk[q] = pre0[q];
+            asm volatile("" : "+v"(pk[q]));
+          }
+        } else {
+          scale_products(pk, err[p], true, gexp, glog, tower);
+        }
+#else
         scale_products(pk, err[p], true, gexp, glog, tower);
+#endif
         mul_acc<4>(out, w, pk);
       }
 #pragma unroll
@@ -325,7 +350,19 @@ __global__ __launch_bounds__(1 << (LGN - 1)) void k_rs_decode_gf16(uint8_t* __re
         w[j] = planes[j * n + swz(p)];
         out[j] = 0;
       }
+#if CEL_D16_PREG
+      if (h == 0) {
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          pk[q] = post0[q];
+          asm volatile("" : "+v"(pk[q]));
+        }
+      } else {
+        scale_products(pk, err[p], false, gexp, glog, tower);
+      }
+#else
       scale_products(pk, err[p], false, gexp, glog, tower);
+#endif
       mul_acc<4>(out, w, pk);
       bs::tr8<0>(out);
       bs::tr8<8>(out);
