@@ -175,10 +175,11 @@ __device__ __forceinline__ void transform(uint32_t* planes, const uint32_t* __re
 // n = 1024: two workgroups per CU. (Keeping the per-point products in LDS, computed once
 // per workgroup instead of once per chunk, takes 101 KiB and one workgroup per CU:
 // 17 % slower, profiles/r3_decode_gf16_ab.txt.)
-// CEL_D16_PREG (A/B knob): keep the per-point products of a thread's first present and
-// first erased point in registers across its chunks instead of recomputing them per chunk.
+// CEL_D16_PREG (A/B knob, default on): keep the per-point products of a thread's first
+// present and first erased point in registers across its chunks instead of recomputing
+// them per chunk: k=512 decode 1.30 -> 1.10 ms (profiles/r3_decode_gf16_preg_ab.txt).
 #ifndef CEL_D16_PREG
-#define CEL_D16_PREG 0
+#define CEL_D16_PREG 1
 #endif
 template <int LGN>
 constexpr size_t decode_gf16_lds() {

@@ -98,3 +98,45 @@ def test_device_limits(ctx):
     z = np.zeros(64, np.uint8).ctypes.data_as(ctypes.c_void_p)
     st = ctx.lib.cel_extend_shares(ctx.handle, z, k * k, 512, None, z, z, z, 0)
     assert st == _lib.ETOOBIG
+
+
+@pytest.mark.parametrize("n", [256, 512, 1024])
+def test_dev_decode_gf16_axes(ctx, oracle, n):
+    """cel_dev_decode over many GF(2^16) axes at once (the bit-plane decoder, 2n = 512..2048
+    points, 512-byte shards = 8 chunks per axis), each axis with its own erasure pattern:
+    one cell lost, exactly n lost, all data lost, all parity lost, and random counts in
+    between, so the present/erased point order of every workgroup takes every shape."""
+    import ctypes
+    from hipmem import DeviceBuffer, synchronize
+    from celestia_eds import _lib
+    rng = np.random.default_rng(7 * n)
+    ln = 512 if n <= 512 else 128
+    naxes = 6 if n <= 512 else 3
+    cws, masks = [], []
+    for a in range(naxes):
+        data = rng.integers(0, 256, (n, ln), dtype=np.uint8)
+        cws.append(np.concatenate([data, oracle.rs_encode(data)]))
+        present = np.ones(2 * n, np.uint8)
+        kind = a % 6
+        if kind == 0:
+            present[rng.integers(0, 2 * n)] = 0
+        elif kind == 1:
+            present[rng.choice(2 * n, n, replace=False)] = 0
+        elif kind == 2:
+            present[:n] = 0
+        elif kind == 3:
+            present[n:] = 0
+        else:
+            present[rng.choice(2 * n, int(rng.integers(1, n + 1)), replace=False)] = 0
+        masks.append(present)
+    cw = np.stack(cws)
+    pres = np.stack(masks)
+    buf = np.where(pres[..., None] == 1, cw, rng.integers(0, 256, cw.shape, dtype=np.uint8)).astype(np.uint8)
+    d, dp = DeviceBuffer(buf.nbytes), DeviceBuffer(pres.nbytes)
+    d.upload(np.ascontiguousarray(buf))
+    dp.upload(np.ascontiguousarray(pres))
+    assert ctx.lib.cel_dev_decode(ctx.handle, d.ptr, dp.ptr, naxes, n, ln, None) == _lib.OK
+    synchronize()
+    out = d.download(buf.shape)
+    for a in range(naxes):
+        assert np.array_equal(out[a], cw[a]), (n, a)
