@@ -265,14 +265,16 @@ __global__ __launch_bounds__(1 << (LGN - 1)) void k_rs_decode_gf16(uint8_t* __re
     // present points are scaled by exp(err), erased ones unscaled by exp(-err)
     err[i] = pres[i] ? e : (kMod16 - e) % kMod16;
   }
-#if CEL_D16_PREG
   // the first present and the first erased point of this thread keep their products in
-  // registers across the chunks (the others, if any, look theirs up per chunk)
-  __syncthreads();
+  // registers across the chunks (the others, if any, look theirs up per chunk); not at
+  // n = 2048, whose 1024-thread workgroups have 128 VGPRs and would spill them
+  constexpr bool PREG = CEL_D16_PREG && LGN <= 10;
   uint32_t pre0[8], post0[8];
-  if (t < np) scale_products(pre0, err[order[t]], true, gexp, glog, tower);
-  if (np + t < n) scale_products(post0, err[order[np + t]], false, gexp, glog, tower);
-#endif
+  if constexpr (PREG) {
+    __syncthreads();
+    if (t < np) scale_products(pre0, err[order[t]], true, gexp, glog, tower);
+    if (np + t < n) scale_products(post0, err[order[np + t]], false, gexp, glog, tower);
+  }
   for (uint32_t chunk = blockIdx.y; chunk < len / 64u; chunk += gridDim.y) {
     const uint32_t coff = chunk * 64u;
     __syncthreads();  // the previous chunk's stores (and the setup) are done with the LDS
@@ -293,8 +295,7 @@ __global__ __launch_bounds__(1 << (LGN - 1)) void k_rs_decode_gf16(uint8_t* __re
         }
         bs::tr8<0>(w);
         bs::tr8<8>(w);
-#if CEL_D16_PREG
-        if (h == 0) {
+        if (PREG && h == 0) {
 #pragma unroll
           for (int q = 0; q < 8; q++) {  // opaque: else the masks are hoisted out of the loop
             pk[q] = pre0[q];
@@ -303,9 +304,6 @@ __global__ __launch_bounds__(1 << (LGN - 1)) void k_rs_decode_gf16(uint8_t* __re
         } else {
           scale_products(pk, err[p], true, gexp, glog, tower);
         }
-#else
-        scale_products(pk, err[p], true, gexp, glog, tower);
-#endif
         mul_acc<4>(out, w, pk);
       }
 #pragma unroll
@@ -351,8 +349,7 @@ __global__ __launch_bounds__(1 << (LGN - 1)) void k_rs_decode_gf16(uint8_t* __re
         w[j] = planes[j * n + swz(p)];
         out[j] = 0;
       }
-#if CEL_D16_PREG
-      if (h == 0) {
+      if (PREG && h == 0) {
 #pragma unroll
         for (int q = 0; q < 8; q++) {
           pk[q] = post0[q];
@@ -361,9 +358,6 @@ __global__ __launch_bounds__(1 << (LGN - 1)) void k_rs_decode_gf16(uint8_t* __re
       } else {
         scale_products(pk, err[p], false, gexp, glog, tower);
       }
-#else
-      scale_products(pk, err[p], false, gexp, glog, tower);
-#endif
       mul_acc<4>(out, w, pk);
       bs::tr8<0>(out);
       bs::tr8<8>(out);
