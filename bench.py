@@ -48,6 +48,12 @@ SHA_MIX_CEILING = 1024 * 2.4e9 * 64 / 4528
 # registers on every lane, no memory traffic, 4-32 waves per SIMD: 29.1-29.6 G
 # compressions/s on two boxes (tools/microbench/sha_rate.hip, profiles/r2_sha_rate.txt).
 SHA_MEASURED_PEAK = 29.4e9
+# The MI355X_MICROARCH.md issue model: every wave64 VALU instruction issues over 2 cycles on
+# a SIMD-32; the compression is 1414 VALU per wave (ISA of the unrolled compression,
+# tools/roofline_crosscheck.py) -> 1024 SIMDs x 2.4 GHz x 64 / (2 x 1414) = 55.6 G/s. The
+# measured per-op rates put v_alignbit / v_add3 (57 % of the mix) at 4 cycles, hence
+# peak_model and the measured peak below it.
+SHA_GUIDE_CEILING = 1024 * 2.4e9 * 64 / (2 * 1414)
 # Measured HBM traffic of the RS extension (rocprofv3 FETCH_SIZE/WRITE_SIZE passes).
 # (input layout -> profile): ODS in Q0 of the EDS (in place) / separate ODS buffer.
 TRAFFIC_PROFILE = {"eds": "r3_rs_traffic_inplace.json", "ods": "r1_rs_traffic.json"}
@@ -200,6 +206,39 @@ def _cpu_cores():
         pass
     # the GPU box grants a CPU share (OMP_NUM_THREADS) far below the visible core count
     return min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+
+
+def cpu_info():
+    """The host the CPU baseline ran on (every report prints the core count
+    and the CPU model): model name, the machine's logical CPUs and physical cores (distinct
+    (package, core id) pairs in /proc/cpuinfo), the CPUs this process may run on and how many
+    physical cores they span, and the thread count the baseline used (the granted share)."""
+    model, cpu_core, cur = None, {}, {}
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                key, _, val = line.partition(":")
+                key, val = key.strip(), val.strip()
+                if key == "model name" and model is None:
+                    model = val
+                if key in ("processor", "physical id", "core id"):
+                    cur[key] = val
+                if not line.strip() and "processor" in cur:
+                    cpu_core[int(cur["processor"])] = (cur.get("physical id", "0"), cur.get("core id", cur["processor"]))
+                    cur = {}
+        if "processor" in cur:
+            cpu_core[int(cur["processor"])] = (cur.get("physical id", "0"), cur.get("core id", cur["processor"]))
+    except OSError:
+        pass
+    try:
+        allowed = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        allowed = list(range(os.cpu_count() or 1))
+    return {"cpu_model": model, "logical_cpus": os.cpu_count(),
+            "physical_cores": len(set(cpu_core.values())) or None,
+            "allowed_cpus": len(allowed),
+            "allowed_physical_cores": len({cpu_core[c] for c in allowed if c in cpu_core}) or None,
+            "granted_threads": _cpu_cores()}
 
 
 def run_sharded(a):
@@ -444,7 +483,7 @@ def run_repair(a):
                          "kind": "port",
                          "sample": f"{n_cpu} repairs of the same damaged square, one per thread (C restatement: "
                                    "crossword sweeps, Leopard FWHT decoder, re-encode and root checks)",
-                         "one_thread_ms_per_repair": t_one * 1e3},
+                         "one_thread_ms_per_repair": t_one * 1e3, **cpu_info()},
         "byzantine": byz,
     }), flush=True)
 
@@ -558,6 +597,7 @@ def cpu_baseline_batch(k, distinct, dah_dev, seconds):
                   f"GFNI/AVX2 Leopard + SHA-NI C restatement, reference tree count)",
         "component_rates_1thread": rates,
         "predicted_from_components": cores / per_sq,
+        **cpu_info(),
     }, parity
 
 
@@ -895,6 +935,10 @@ def main():
             "peak_model": SHA_MIX_CEILING / 1e9,
             "frac_model": nmt_rate / SHA_MIX_CEILING,
             "peak_model_basis": "SHA-256 instruction mix at measured per-op VALU rates (profiles/r1_microbench_valu.txt)",
+            "peak_guide": SHA_GUIDE_CEILING / 1e9,
+            "frac_guide": nmt_rate / SHA_GUIDE_CEILING,
+            "peak_guide_basis": "1414 VALU per compression x 2 cycles per wave64 instruction (MI355X_MICROARCH.md "
+                                "issue model), 1024 SIMDs, 2.4 GHz",
             "avg_launch_us": t_com * 1e6,
         },
     }

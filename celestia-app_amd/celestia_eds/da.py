@@ -45,21 +45,40 @@ def _is_pow2(n):
     return n > 0 and (n & (n - 1)) == 0
 
 
-def _extend(shares, ctx=None, order_check=True):
-    ctx = ctx or _lib.default_context()
+def _ods_buffer(shares):
+    """The share list (or an (n, share_size) array) of ExtendShares as one contiguous
+    buffer, with the checks the C side cannot make (it receives only n and the share size):
+    data_availability_header.go:67-69's power-of-two count, and rsmt2d's equal chunk sizes
+    (newDataSquare [dep]: every chunk as long as the first). A share size other than 512
+    then gets the library's own ECHUNK. Returns (ods, n, share_size)."""
     n = len(shares)
     if not _is_pow2(n):
         raise CelError(_lib.ENOTPOW2, f"number of shares is not a power of 2: got {n}")
     if isinstance(shares, np.ndarray):
+        if shares.ndim != 2:
+            raise CelError(_lib.EINVAL, f"shares must be an (n, share_size) array: got shape {shares.shape}")
         ods = np.ascontiguousarray(shares, np.uint8).reshape(-1)
+        size = shares.shape[1]
     else:
-        ods = np.frombuffer(b"".join(bytes(s) for s in shares), np.uint8).copy()
+        chunks = [bytes(s) for s in shares]
+        size = len(chunks[0])
+        if any(len(c) != size for c in chunks):
+            raise CelError(_lib.ECHUNK, "non-nil chunks not all of equal size")
+        ods = np.frombuffer(b"".join(chunks), np.uint8).copy()
+    if ods.size != n * size:
+        raise CelError(_lib.EINVAL, f"share buffer holds {ods.size} bytes, not {n} x {size}")
+    return ods, n, size
+
+
+def _extend(shares, ctx=None, order_check=True):
+    ods, n, size = _ods_buffer(shares)  # input errors before any device is touched
+    ctx = ctx or _lib.default_context()
     k = SquareSize(n)
     eds = np.zeros((2 * k, 2 * k, SHARE_SIZE), np.uint8)
     rr = np.zeros((2 * k, _lib.NMT_NODE_SIZE), np.uint8)
     cr = np.zeros((2 * k, _lib.NMT_NODE_SIZE), np.uint8)
     dah = np.zeros(32, np.uint8)
-    ctx.check(ctx.lib.cel_extend_shares(ctx.handle, _p(ods), n, SHARE_SIZE, _p(eds), _p(rr), _p(cr), _p(dah),
+    ctx.check(ctx.lib.cel_extend_shares(ctx.handle, _p(ods), n, size, _p(eds), _p(rr), _p(cr), _p(dah),
                                         _lib.FLAG_ORDER_CHECK if order_check else 0))
     out = ExtendedDataSquare(eds, rr, cr, ctx=ctx)
     out._dah = dah.tobytes()
@@ -77,19 +96,13 @@ def ComputeDataAvailabilityHeader(shares, ctx=None):
     build the DAH and use nothing but dah.Hash() ("the eds is not returned here"). One
     device pass with no EDS copied back (cel_extend_shares with eds_out = NULL): the ODS
     goes up, the 4k roots and the hash come down. Same errors as ExtendShares."""
+    ods, n, size = _ods_buffer(shares)  # input errors before any device is touched
     ctx = ctx or _lib.default_context()
-    n = len(shares)
-    if not _is_pow2(n):
-        raise CelError(_lib.ENOTPOW2, f"number of shares is not a power of 2: got {n}")
-    if isinstance(shares, np.ndarray):
-        ods = np.ascontiguousarray(shares, np.uint8).reshape(-1)
-    else:
-        ods = np.frombuffer(b"".join(bytes(s) for s in shares), np.uint8).copy()
     k = SquareSize(n)
     rr = np.zeros((2 * k, _lib.NMT_NODE_SIZE), np.uint8)
     cr = np.zeros((2 * k, _lib.NMT_NODE_SIZE), np.uint8)
     dah = np.zeros(32, np.uint8)
-    ctx.check(ctx.lib.cel_extend_shares(ctx.handle, _p(ods), n, SHARE_SIZE, None, _p(rr), _p(cr), _p(dah),
+    ctx.check(ctx.lib.cel_extend_shares(ctx.handle, _p(ods), n, size, None, _p(rr), _p(cr), _p(dah),
                                         _lib.FLAG_ORDER_CHECK))
     out = DataAvailabilityHeader([r.tobytes() for r in rr], [c.tobytes() for c in cr])
     out.hash = dah.tobytes()

@@ -185,13 +185,7 @@ cel_status cel_device_name(cel_ctx* ctx, char* buf, size_t len) {
 // tree top + DAH runs beside the other's work. Two chunks (profiles/r1g_pipe_chunks_ab.txt);
 // chaining the extensions so each runs beside the previous chunk's hashing buys nothing,
 // the step is the sum of the two VALU-bound phases (profiles/r2_pipe_overlap_ab.txt).
-#ifndef CEL_PIPE_CHUNKS
-#define CEL_PIPE_CHUNKS 2
-#endif
-#ifndef CEL_PIPE_CHAIN
-#define CEL_PIPE_CHAIN 0
-#endif
-constexpr uint32_t kPipeChunks = CEL_PIPE_CHUNKS;
+constexpr uint32_t kPipeChunks = 2;
 
 static void pipe_plan(uint32_t n, uint32_t* chunk, uint32_t* nchunks) {
   uint32_t nc = n < kPipeChunks ? n : kPipeChunks;
@@ -292,7 +286,6 @@ cel_status cel_dev_extend_batch(cel_ctx* ctx, const void* d_ods, uint32_t n, uin
     const uint32_t first = c * chunk, cnt = (first + chunk <= n) ? chunk : n - first;
     hipStream_t s = ctx->sub[c % cel_ctx::kPipe];
     if ((e = hipStreamWaitEvent(s, ctx->ev_start, 0)) != hipSuccess) break;
-    if (CEL_PIPE_CHAIN && c > 0 && (e = hipStreamWaitEvent(s, ctx->ev_rs[c - 1], 0)) != hipSuccess) break;
     const uint8_t* ods = d_ods ? static_cast<const uint8_t*>(d_ods) + first * ods_sq : nullptr;
     uint8_t* eds = static_cast<uint8_t*>(d_eds) + first * eds_sq;
     if ((e = launch_extend(ods, eds, k, cnt, ctx->tables, s)) != hipSuccess) break;
@@ -1267,9 +1260,6 @@ static cel_status fail_axis(cel_ctx* ctx, const RepairBufs& b, const std::vector
                              : std::string("byzantine ") + (is_col ? "column" : "row") + " " + std::to_string(idx));
 }
 
-#ifndef CEL_REPAIR_CHECKS_FIRST
-#define CEL_REPAIR_CHECKS_FIRST 1
-#endif
 // Commit every root of the square on the main stream beside the side stream's last checks,
 // join the streams and read roots and flags back (one page-locked copy).
 static cel_status verify_square(cel_ctx* ctx, RepairBufs& b, uint32_t k, int last_col, const Issued& last,
@@ -1281,15 +1271,12 @@ static cel_status verify_square(cel_ctx* ctx, RepairBufs& b, uint32_t k, int las
   if ((st = fuzz(ctx, b.main)) != CEL_OK) return st;
   // the last pass's checks go to the side stream ahead of the commit's dozen launches, so
   // they run beside its leaf hashing instead of trailing its tree levels
-  if (CEL_REPAIR_CHECKS_FIRST && ((st = solve_check(ctx, b, k, last_col, last)) != CEL_OK ||
-                                  (st = check_pass(ctx, b, k, pending_col, pending, false)) != CEL_OK))
+  if ((st = solve_check(ctx, b, k, last_col, last)) != CEL_OK ||
+      (st = check_pass(ctx, b, k, pending_col, pending, false)) != CEL_OK)
     return st;
   if ((e = launch_commit(b.eds, k, 1, b.roots, b.roots + roots_b, nullptr, nullptr, b.work, false, b.main)) !=
       hipSuccess)
     return hip_fail(ctx, e, "roots");
-  if (!CEL_REPAIR_CHECKS_FIRST && ((st = solve_check(ctx, b, k, last_col, last)) != CEL_OK ||
-                                   (st = check_pass(ctx, b, k, pending_col, pending, false)) != CEL_OK))
-    return st;
   if ((e = hipEventRecord(b.ev_done, b.side)) != hipSuccess || (e = hipStreamWaitEvent(b.main, b.ev_done, 0)) != hipSuccess)
     return hip_fail(ctx, e, "join");
   if ((e = hipMemcpyAsync(b.hres, b.roots, b.res_bytes, hipMemcpyDeviceToHost, b.main)) != hipSuccess)
@@ -1627,7 +1614,8 @@ static cel_status repair_core(cel_ctx* ctx, RepairBufs& b, std::vector<uint8_t>&
         solves.push_back({is_col, list[t]});
       }
       std::sort(orth.begin(), orth.end());
-      if (!pending.empty() && (st = check_pass(ctx, b, k, pending_col, pending, false)) != CEL_OK) return st;
+      // pending is empty here: the previous pass's orthogonal checks were issued (and
+      // cleared) right after this pass's solve above, or this is the first pass
       pending.swap(orth);
       pending_col = !is_col;
       progress = true;

@@ -22,24 +22,6 @@
 #include "cel_internal.hpp"
 #include "sha256_device.hpp"
 
-// Minimum waves per SIMD requested from the register allocator (0 = compiler default).
-#ifndef CEL_LEAF_WAVES
-#define CEL_LEAF_WAVES 0
-#endif
-#ifndef CEL_LEVEL_WAVES
-#define CEL_LEVEL_WAVES 0
-#endif
-#if CEL_LEAF_WAVES > 0
-#define CEL_LEAF_BOUNDS __launch_bounds__(256, CEL_LEAF_WAVES)
-#else
-#define CEL_LEAF_BOUNDS __launch_bounds__(256)
-#endif
-#if CEL_LEVEL_WAVES > 0
-#define CEL_LEVEL_BOUNDS __launch_bounds__(256, CEL_LEVEL_WAVES)
-#else
-#define CEL_LEVEL_BOUNDS __launch_bounds__(256)
-#endif
-
 namespace cel {
 
 struct Node {
@@ -214,7 +196,7 @@ __device__ __forceinline__ void make_leaf_node(const uint32_t* __restrict__ sh, 
 
 // grid: x = cell block (256 cells), y = square. Writes leaf nodes [sq][W*W][24].
 template <bool ORDER, bool PF>
-__global__ CEL_LEAF_BOUNDS void k_leaf(const uint8_t* __restrict__ eds, uint32_t k, uint32_t* __restrict__ leaves,
+__global__ __launch_bounds__(256) void k_leaf(const uint8_t* __restrict__ eds, uint32_t k, uint32_t* __restrict__ leaves,
                                               int32_t* __restrict__ bad_axis) {
   const uint32_t W = 2 * k;
   const uint32_t cell = blockIdx.x * 256u + threadIdx.x;
@@ -258,9 +240,6 @@ __device__ __forceinline__ uint32_t node_word(const uint32_t (&L)[kNodeWords], c
   return 0u;
 }
 
-// UNR: blocks 1 and 2 with every round unrolled (latency-bound levels: a few waves per
-// SIMD, one node per lane, so the rolled loop's overhead sits on the chain).
-template <bool UNR = false>
 __device__ __forceinline__ void hash_node(const uint32_t (&L)[kNodeWords], const uint32_t (&R)[kNodeWords],
                                           uint32_t (&out)[kNodeWords]) {
   uint32_t st[8];
@@ -287,8 +266,7 @@ __device__ __forceinline__ void hash_node(const uint32_t (&L)[kNodeWords], const
     uint32_t w[16];
 #pragma unroll
     for (int wi = 0; wi < 16; wi++) w[wi] = node_word(L, R, 16 * b + wi);
-    if (UNR) sha256_compress_unrolled(st, w);
-    else sha256_compress(st, w);
+    sha256_compress(st, w);
   }
   bool rpar = (R[7] & 0xFFu) == 0xFFu;
 #pragma unroll
@@ -314,8 +292,8 @@ __device__ __forceinline__ void rfc_leaf90(const uint32_t (&R)[kNodeWords], uint
 // 90 bytes, straight into the caller's row_out / col_out ([nsq][W][90]); with
 // leafd != nullptr it also hashes the root as an RFC-6962 leaf of the DAH tree
 // (2 compressions) so the per-square DAH kernel starts from leaf digests.
-template <bool FROM_LEAVES, bool UNR = false>
-__global__ CEL_LEVEL_BOUNDS void k_level(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint32_t W,
+template <bool FROM_LEAVES>
+__global__ __launch_bounds__(256) void k_level(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint32_t W,
                                                uint32_t nin, uint32_t trees, uint32_t* __restrict__ leafd,
                                                uint8_t* __restrict__ row_out, uint8_t* __restrict__ col_out) {
   const uint32_t nout = nin / 2;
@@ -335,7 +313,7 @@ __global__ CEL_LEVEL_BOUNDS void k_level(const uint32_t* __restrict__ in, uint32
   uint32_t L[kNodeWords], R[kNodeWords], o[kNodeWords];
   load_node(in + li * kNodeWords, L);
   load_node(in + ri * kNodeWords, R);
-  hash_node<UNR>(L, R, o);
+  hash_node(L, R, o);
   const uint64_t oi = (uint64_t)blockIdx.y * trees * nout + idx;
   store_node(out + oi * kNodeWords, o);
   if (row_out) {
@@ -382,9 +360,6 @@ __device__ __forceinline__ void rfc_leaf90(const uint32_t (&R)[kNodeWords], uint
 // innerHash = SHA256(0x01 || l(32) || r(32)) (2 blocks). The DAH tree hashes its levels
 // one after the other in one workgroup (a latency chain), so both compressions are
 // unrolled; the second block's 15 constant words fold into its schedule.
-#ifndef CEL_DAH_UNROLL
-#define CEL_DAH_UNROLL 0
-#endif
 __device__ __forceinline__ void rfc_inner(const uint32_t* l, const uint32_t* r, uint32_t (&st)[8]) {
   uint32_t w[16];
   w[0] = 0x01000000u | (l[0] >> 8);
@@ -399,13 +374,8 @@ __device__ __forceinline__ void rfc_inner(const uint32_t* l, const uint32_t* r, 
 #pragma unroll
   for (int i = 1; i < 15; i++) w2[i] = 0;
   w2[15] = 65u * 8u;
-  if (CEL_DAH_UNROLL) {
-    sha256_compress_unrolled(st, w);
-    sha256_compress_unrolled(st, w2);
-  } else {
-    sha256_compress(st, w);
-    sha256_compress(st, w2);
-  }
+  sha256_compress(st, w);
+  sha256_compress(st, w2);
 }
 
 // SHA256 of the empty string (RFC-6962 empty tree).
@@ -523,11 +493,6 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // latency is then exposed and the prefetching leaf hash (leaf_hash<true>) pays.
 static bool latency_bound(uint64_t lanes) { return lanes <= 2ull * 1024 * 64; }
 
-// Tree levels of at most latency_bound() lanes hash with unrolled compressions (A/B knob).
-#ifndef CEL_LEVEL_UNROLL
-#define CEL_LEVEL_UNROLL 0
-#endif
-
 // Workspace: leaves [nsq][W*W] nodes | ping [nsq][2W][W/2] | pong [nsq][2W][W/4] |
 //            roots [nsq][2W] nodes | bad_axis [nsq] int32 | DAH leaf digests [nsq][2W][8]
 size_t nmt_workspace_size(uint32_t k, uint32_t nsq) {
@@ -582,10 +547,8 @@ hipError_t launch_commit(const uint8_t* eds, uint32_t k, uint32_t nsq, uint8_t* 
     dim3 g((trees * nout + 255) / 256, nsq);
     uint8_t* ro = (nout == 1) ? row_roots : nullptr;
     uint8_t* co = (nout == 1) ? col_roots : nullptr;
-    const bool unr = CEL_LEVEL_UNROLL && latency_bound((uint64_t)trees * nout * nsq);
     if (first) hipLaunchKernelGGL(k_level<true>, g, dim3(256), 0, s, src, out, W, nin, trees, ld, ro, co);
-    else if (unr) hipLaunchKernelGGL((k_level<false, true>), g, dim3(256), 0, s, src, out, W, nin, trees, ld, ro, co);
-    else hipLaunchKernelGGL((k_level<false, false>), g, dim3(256), 0, s, src, out, W, nin, trees, ld, ro, co);
+    else hipLaunchKernelGGL(k_level<false>, g, dim3(256), 0, s, src, out, W, nin, trees, ld, ro, co);
     first = false;
     src = out;
     dst = (dst == ping) ? pong : ping;
@@ -611,7 +574,7 @@ hipError_t launch_commit(const uint8_t* eds, uint32_t k, uint32_t nsq, uint8_t* 
 // combined into the row roots after an all-gather.
 
 template <bool ORDER, bool PF>
-__global__ CEL_LEAF_BOUNDS void k_slab_leaf(const uint8_t* __restrict__ slab, uint32_t k, uint32_t c0, uint32_t w,
+__global__ __launch_bounds__(256) void k_slab_leaf(const uint8_t* __restrict__ slab, uint32_t k, uint32_t c0, uint32_t w,
                                             uint32_t cell0, uint32_t cell1, uint32_t* __restrict__ leaves,
                                             int32_t* __restrict__ bad_axis) {
   const uint32_t W = 2 * k;
@@ -631,7 +594,7 @@ __global__ CEL_LEAF_BOUNDS void k_slab_leaf(const uint8_t* __restrict__ slab, ui
 
 // First tree level over a strided node grid: tree t's leaf l is in[t * tstride + l * lstride].
 // Output compact: out[t][nin / 2].
-__global__ CEL_LEVEL_BOUNDS void k_level_grid(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint32_t nin,
+__global__ __launch_bounds__(256) void k_level_grid(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint32_t nin,
                                               uint32_t trees, uint32_t tstride, uint32_t lstride) {
   const uint32_t nout = nin / 2;
   const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
@@ -654,8 +617,7 @@ struct LevelJob {
   uint32_t nin, trees, tstride, lstride;
 };
 
-template <bool UNR>
-__global__ CEL_LEVEL_BOUNDS void k_level_pair(LevelJob a, LevelJob b) {
+__global__ __launch_bounds__(256) void k_level_pair(LevelJob a, LevelJob b) {
   uint32_t idx = blockIdx.x * 256u + threadIdx.x;
   const uint32_t na = a.nin > 1 ? a.trees * (a.nin / 2) : 0u;
   const uint32_t nb = b.nin > 1 ? b.trees * (b.nin / 2) : 0u;
@@ -668,7 +630,7 @@ __global__ CEL_LEVEL_BOUNDS void k_level_pair(LevelJob a, LevelJob b) {
   uint32_t L[kNodeWords], R[kNodeWords], o[kNodeWords];
   load_node(j.in + li * kNodeWords, L);
   load_node(j.in + ri * kNodeWords, R);
-  hash_node<UNR>(L, R, o);
+  hash_node(L, R, o);
   store_node(j.out + (uint64_t)idx * kNodeWords, o);
 }
 
@@ -768,8 +730,7 @@ static void reduce_grid_pair(LevelJob a, uint32_t* ping_a, uint32_t* pong_a, uin
     if (a.nin > 1) a.out = a.nin == 2 ? roots_a : dst_a;
     if (b.nin > 1) b.out = b.nin == 2 ? roots_b : dst_b;
     const uint32_t n = (a.nin > 1 ? a.trees * (a.nin / 2) : 0u) + (b.nin > 1 ? b.trees * (b.nin / 2) : 0u);
-    if (CEL_LEVEL_UNROLL && latency_bound(n)) hipLaunchKernelGGL(k_level_pair<true>, dim3((n + 255) / 256), dim3(256), 0, s, a, b);
-    else hipLaunchKernelGGL(k_level_pair<false>, dim3((n + 255) / 256), dim3(256), 0, s, a, b);
+    hipLaunchKernelGGL(k_level_pair, dim3((n + 255) / 256), dim3(256), 0, s, a, b);
     if (a.nin > 1) {
       a.in = a.out;
       a.nin /= 2;

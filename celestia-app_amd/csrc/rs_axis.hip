@@ -50,18 +50,9 @@ constexpr uint32_t merged_lm(uint32_t s1, uint32_t s2) {
 // multiply (~10 VALU per dword). Layers D = 1, 2, 4 (twiddles differ inside a block) keep
 // the v_perm multiply. For K = 128: 6 v_perm layers, 7 bit-sliced layers, 32 transposes.
 
-// Scheduling fence in the v_perm layers every CEL_AX_SB butterflies (A/B knob; 1 = after
-// every butterfly, 0 = none: the compiler may interleave a whole layer).
-#ifndef CEL_AX_SB
-#define CEL_AX_SB 1
-#endif
-#ifndef CEL_AX_LDS
-#define CEL_AX_LDS 0
-#endif
-template <int J>
-__device__ __forceinline__ void vperm_fence() {
-  if constexpr (CEL_AX_SB > 0 && (J + 1) % (CEL_AX_SB > 0 ? CEL_AX_SB : 1) == 0) __builtin_amdgcn_sched_barrier(0);
-}
+// Scheduling fence after every v_perm butterfly (a fence every 2 or 4 butterflies, or
+// none, measured within noise: profiles/r3_gf8_fence_ab.txt).
+__device__ __forceinline__ void vperm_fence() { __builtin_amdgcn_sched_barrier(0); }
 
 template <int K>
 __device__ __forceinline__ void transform_hyb(uint32_t (&w)[K]) {
@@ -80,7 +71,7 @@ __device__ __forceinline__ void transform_hyb(uint32_t (&w)[K]) {
         w[a + D] ^= w[a];
         m.muladd(w[a], w[a + D], m7, m3);
         pin(w[a], w[a + D]);
-        vperm_fence<base / 2 + decltype(j)::value>();
+        vperm_fence();
       });
     });
   });
@@ -140,7 +131,7 @@ __device__ __forceinline__ void transform_hyb(uint32_t (&w)[K]) {
         m.muladd(w[a], w[a + D], m7, m3);
         w[a + D] ^= w[a];
         pin(w[a], w[a + D]);
-        vperm_fence<base / 2 + decltype(j)::value>();
+        vperm_fence();
       });
     });
   });
@@ -193,9 +184,7 @@ hipError_t launch(const RsGeom& g, hipStream_t s) {
   const uint64_t ntiles = (uint64_t)g.axes * nslice * g.nsq;
   if (ntiles == 0) return hipSuccess;
   if (ntiles > 0xFFFFFFF0ull) return hipErrorInvalidValue;
-  // CEL_AX_LDS (A/B knob, default 0): dynamic LDS per workgroup that caps the RS
-  // workgroups per CU (160 KiB / CEL_AX_LDS), leaving register room for NMT waves beside them
-  hipLaunchKernelGGL(k_rs_axis_gf8<LOGK>, dim3((unsigned)((ntiles + 3) / 4)), dim3(256), CEL_AX_LDS, s, g, nslice);
+  hipLaunchKernelGGL(k_rs_axis_gf8<LOGK>, dim3((unsigned)((ntiles + 3) / 4)), dim3(256), 0, s, g, nslice);
   return hipGetLastError();
 }
 

@@ -102,11 +102,7 @@ __device__ __forceinline__ void scale_products(uint32_t (&pk)[8], uint32_t e, bo
 // layer's x (or y) points seen by 32 lanes of a ds_read_b32 group differ in 5 of the bits
 // 0-5 of p, so they fall on 32 distinct banks ((word mod 32)) for every D: without the
 // flip D = 1..16 were 2-way conflicts.
-// (CEL_D16_SWZ=0: the plain layout, for A/B runs.)
-#ifndef CEL_D16_SWZ
-#define CEL_D16_SWZ 1
-#endif
-__device__ __forceinline__ uint32_t swz(uint32_t p) { return CEL_D16_SWZ ? p ^ ((0u - ((p >> 5) & 1u)) & 31u) : p; }
+__device__ __forceinline__ uint32_t swz(uint32_t p) { return p ^ ((0u - ((p >> 5) & 1u)) & 31u); }
 
 template <int LGN, bool IFFT, int J, bool UNI>
 __device__ __forceinline__ void layer(uint32_t* planes, const uint32_t* __restrict__ tw, uint32_t t, uint32_t ld,
@@ -175,12 +171,9 @@ __device__ __forceinline__ void transform(uint32_t* planes, const uint32_t* __re
 // n = 1024: two workgroups per CU. (Keeping the per-point products in LDS, computed once
 // per workgroup instead of once per chunk, takes 101 KiB and one workgroup per CU:
 // 17 % slower, profiles/r3_decode_gf16_ab.txt.)
-// CEL_D16_PREG (A/B knob, default on): keep the per-point products of a thread's first
-// present and first erased point in registers across its chunks instead of recomputing
-// them per chunk: k=512 decode 1.30 -> 1.10 ms (profiles/r3_decode_gf16_preg_ab.txt).
-#ifndef CEL_D16_PREG
-#define CEL_D16_PREG 1
-#endif
+// The per-point products of a thread's first present and first erased point stay in
+// registers across its chunks instead of being recomputed per chunk: k=512 decode 1.30 ->
+// 1.10 ms (profiles/r3_decode_gf16_preg_ab.txt).
 template <int LGN>
 constexpr size_t decode_gf16_lds() {
   constexpr size_t n = size_t(1) << LGN;
@@ -268,7 +261,7 @@ __global__ __launch_bounds__(1 << (LGN - 1)) void k_rs_decode_gf16(uint8_t* __re
   // the first present and the first erased point of this thread keep their products in
   // registers across the chunks (the others, if any, look theirs up per chunk); not at
   // n = 2048, whose 1024-thread workgroups have 128 VGPRs and would spill them
-  constexpr bool PREG = CEL_D16_PREG && LGN <= 10;
+  constexpr bool PREG = LGN <= 10;
   uint32_t pre0[8], post0[8];
   if constexpr (PREG) {
     __syncthreads();

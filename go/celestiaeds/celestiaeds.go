@@ -67,6 +67,35 @@ func tooBig(err error) bool {
 	return errors.As(err, &se) && se.Status == C.CEL_ETOOBIG
 }
 
+// deviceCodec reports whether codec computes what the device computes: Leopard parity
+// (rsmt2d.NewLeoRSCodec, appconsts.DefaultCodec at pkg/appconsts/global_consts.go:92;
+// cel_codec_name() is "Leopard"). Any other rsmt2d.Codec gets the reference path, so its
+// parity and roots are that codec's.
+func deviceCodec(codec rsmt2d.Codec) bool {
+	return codec != nil && codec.Name() == C.GoString(C.cel_codec_name())
+}
+
+// deviceShares reports whether every share is appconsts.ShareSize bytes, the only share
+// size the device path takes (the C ABI receives n and the size, never the lengths). Other
+// lengths go to rsmt2d, which extends any equal, 64-byte-multiple chunk size and returns
+// its own error for the rest.
+func deviceShares(shares [][]byte) bool {
+	for _, s := range shares {
+		if len(s) != ShareSize {
+			return false
+		}
+	}
+	return true
+}
+
+func squareWidth(n int) int {
+	k := 1
+	for k*k < n {
+		k <<= 1
+	}
+	return k
+}
+
 type Context struct {
 	mu  sync.Mutex
 	ctx *C.cel_ctx
@@ -107,6 +136,10 @@ func (c *Context) errLocked(st C.cel_status) error {
 // one call. A caller can wrap flat with rsmt2d.ImportExtendedDataSquare(cells of flat,
 // codec, (&RootTable{...}).NewTree). ExtendSquare does that with less PCIe traffic.
 func (c *Context) ExtendShares(shares [][]byte) (flat []byte, rowRoots, colRoots [][]byte, dah []byte, err error) {
+	if !deviceShares(shares) {
+		return nil, nil, nil, nil, &StatusError{Status: C.CEL_ECHUNK,
+			Msg: fmt.Sprintf("every share must be %d bytes on the device path", ShareSize)}
+	}
 	return c.extend(shares, flagOrder)
 }
 
@@ -121,11 +154,7 @@ func (c *Context) extend(shares [][]byte, flags C.uint32_t) (flat []byte, rowRoo
 	for i, s := range shares {
 		copy(dst[i*ShareSize:], s)
 	}
-	k := 1
-	for k*k < n {
-		k <<= 1
-	}
-	w := 2 * k
+	w := 2 * squareWidth(n)
 	flat = make([]byte, w*w*ShareSize)
 	rr := make([]byte, w*NmtNodeSize)
 	cr := make([]byte, w*NmtNodeSize)
@@ -149,20 +178,20 @@ func (c *Context) extend(shares [][]byte, flags C.uint32_t) (flat []byte, rowRoo
 // the same power-of-two check and error, then one device pass, and an
 // *rsmt2d.ExtendedDataSquare imported with a RootTable constructor, so
 // da.NewDataAvailabilityHeader's eds.RowRoots()/ColRoots() return the device roots.
-// A square wider than the device path (CEL_ETOOBIG: k > 512) is extended by the
-// reference call itself, rsmt2d.ComputeExtendedDataSquare with wrapper.NewConstructor,
-// exactly as data_availability_header.go:74 does: the domain stays the reference's.
+// A square wider than the device path (CEL_ETOOBIG: k > 512), and a codec other than
+// Leopard, are extended by the reference call itself, rsmt2d.ComputeExtendedDataSquare
+// with wrapper.NewConstructor, exactly as data_availability_header.go:74 does: the domain
+// and the codec stay the reference's.
 func (c *Context) ExtendSquare(shares [][]byte, codec rsmt2d.Codec) (*rsmt2d.ExtendedDataSquare, error) {
 	if n := len(shares); n == 0 || n&(n-1) != 0 {
 		return nil, fmt.Errorf("number of shares is not a power of 2: got %d", n)
 	}
+	if !deviceCodec(codec) || !deviceShares(shares) {
+		return rsmt2d.ComputeExtendedDataSquare(shares, codec, wrapper.NewConstructor(uint64(squareWidth(len(shares)))))
+	}
 	flat, rr, cr, _, err := c.extend(shares, flagOrder|flagParity)
 	if tooBig(err) {
-		k := 1
-		for k*k < len(shares) {
-			k <<= 1
-		}
-		return rsmt2d.ComputeExtendedDataSquare(shares, codec, wrapper.NewConstructor(uint64(k)))
+		return rsmt2d.ComputeExtendedDataSquare(shares, codec, wrapper.NewConstructor(uint64(squareWidth(len(shares)))))
 	}
 	if err != nil {
 		return nil, err
@@ -186,16 +215,29 @@ func (c *Context) ExtendSquare(shares [][]byte, codec rsmt2d.Codec) (*rsmt2d.Ext
 // app/process_proposal.go:138-156 use nothing but dah.Hash() ("the eds is not returned
 // here"). One device pass with no EDS copied back (cel_extend_shares, eds_out = NULL): 8 MiB
 // up and 46 KB of roots down for k = 128 instead of 8 MiB up and 24 MiB down. Outside the
-// device's domain (CEL_ETOOBIG) the reference computes it: rsmt2d.ComputeExtendedDataSquare
-// with wrapper.NewConstructor, then the square's RowRoots / ColRoots.
+// device's domain (CEL_ETOOBIG), or with a codec other than Leopard, the reference computes
+// it: rsmt2d.ComputeExtendedDataSquare with wrapper.NewConstructor, then the square's
+// RowRoots / ColRoots.
 func (c *Context) DataAvailabilityHeader(shares [][]byte, codec rsmt2d.Codec) (rowRoots, colRoots [][]byte, err error) {
 	n := len(shares)
 	if n == 0 || n&(n-1) != 0 {
 		return nil, nil, fmt.Errorf("number of shares is not a power of 2: got %d", n)
 	}
-	k := 1
-	for k*k < n {
-		k <<= 1
+	k := squareWidth(n)
+	reference := func() ([][]byte, [][]byte, error) {
+		eds, cerr := rsmt2d.ComputeExtendedDataSquare(shares, codec, wrapper.NewConstructor(uint64(k)))
+		if cerr != nil {
+			return nil, nil, cerr
+		}
+		rows, rerr := eds.RowRoots()
+		if rerr != nil {
+			return nil, nil, rerr
+		}
+		cols, cerr := eds.ColRoots()
+		return rows, cols, cerr
+	}
+	if !deviceCodec(codec) || !deviceShares(shares) {
+		return reference()
 	}
 	buf := C.malloc(C.size_t(n * ShareSize))
 	defer C.free(buf)
@@ -213,15 +255,7 @@ func (c *Context) DataAvailabilityHeader(shares [][]byte, codec rsmt2d.Codec) (r
 			(*C.uint8_t)(unsafe.Pointer(&dah[0])), flagOrder)
 	})
 	if tooBig(err) {
-		eds, cerr := rsmt2d.ComputeExtendedDataSquare(shares, codec, wrapper.NewConstructor(uint64(k)))
-		if cerr != nil {
-			return nil, nil, cerr
-		}
-		if rowRoots, err = eds.RowRoots(); err != nil {
-			return nil, nil, err
-		}
-		colRoots, err = eds.ColRoots()
-		return rowRoots, colRoots, err
+		return reference()
 	}
 	if err != nil {
 		return nil, nil, err
@@ -239,7 +273,9 @@ func (c *Context) DataAvailabilityHeader(shares [][]byte, codec rsmt2d.Codec) (r
 // MaxChunks is the reference's 32768^2; codewords wider than the device kernels (encode
 // n > 2048 data shards, decode n > 1024: CEL_ETOOBIG) go to the reference LeoRSCodec
 // (appconsts.DefaultCodec, global_consts.go:92), so every input the reference accepts
-// is accepted here with the reference's result.
+// is accepted here with the reference's result. So are the inputs the C ABI cannot be
+// handed (no shards, no bytes, shards of unequal lengths, an odd codeword): the reference
+// codec returns its own error for them.
 type Codec struct{ C *Context }
 
 var refCodec = appconsts.DefaultCodec()
@@ -256,7 +292,15 @@ func (cd Codec) ValidateChunkSize(n int) error {
 }
 
 func (cd Codec) Encode(data [][]byte) ([][]byte, error) {
+	if len(data) == 0 || len(data[0]) == 0 {
+		return refCodec.Encode(data)
+	}
 	n, l := len(data), len(data[0])
+	for _, d := range data {
+		if len(d) != l {
+			return refCodec.Encode(data)
+		}
+	}
 	in := C.malloc(C.size_t(n * l))
 	out := C.malloc(C.size_t(n * l))
 	defer C.free(in)
@@ -287,6 +331,14 @@ func (cd Codec) Decode(shards [][]byte) ([][]byte, error) {
 		if s != nil {
 			l = len(s)
 			break
+		}
+	}
+	if n2 == 0 || n2%2 != 0 || l == 0 {
+		return refCodec.Decode(shards)
+	}
+	for _, s := range shards {
+		if s != nil && len(s) != l {
+			return refCodec.Decode(shards)
 		}
 	}
 	buf := C.malloc(C.size_t(n2 * l))
@@ -395,7 +447,9 @@ func (c *Context) GetCommitment(eds []byte, k, start, blobShareLen, subtreeRootT
 // shares a celestia-node bad-encoding fraud proof is built from), the plain "bad root
 // input" error of preRepairSanityCheck, or rsmt2d.ErrUnrepairableDataSquare. On an
 // error present[] is left as the mask the partially repaired flat is valid under.
-// Squares wider than the device path (CEL_ETOOBIG, k > 512) are repaired by rsmt2d itself.
+// Squares wider than the device path (CEL_ETOOBIG, k > 512) are repaired by rsmt2d itself;
+// if that fallback fails, flat and present[] are left exactly as the caller passed them
+// (rsmt2d fills new cell slices, never the known cells it imported from flat).
 func (c *Context) Repair(flat, present []byte, k int, rowRoots, colRoots [][]byte) error {
 	w := 2 * k
 	rr := make([]byte, 0, w*NmtNodeSize)

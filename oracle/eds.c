@@ -411,9 +411,23 @@ int orc_repair(uint8_t* eds, uint8_t* present, uint32_t k, size_t share, const u
  * (or repairs) on independent threads, each single-threaded inside with buffers reused
  * across its squares, the way a node extends one block per goroutine set. Not a checker.
  */
+/* Per-thread scratch that outlives a call (OpenMP keeps its threads across parallel
+ * regions): a fresh 32 MiB EDS per call would be page-faulted in again every time. */
+static __thread uint8_t* tl_buf;
+static __thread size_t tl_cap;
+
+static uint8_t* thread_scratch(size_t bytes) {
+  if (bytes > tl_cap) {
+    free(tl_buf);
+    tl_buf = (uint8_t*)malloc(bytes);
+    tl_cap = tl_buf ? bytes : 0;
+  }
+  return tl_buf;
+}
+
 int orc_extend_commit_many(const uint8_t* ods, uint32_t n, uint32_t k, size_t share, uint8_t* dah_out) {
   orc_init();
-  const size_t ods_b = (size_t)k * k * share, eds_b = 4 * ods_b;
+  const size_t ods_b = (size_t)k * k * share, eds_b = 4 * ods_b, roots_b = (size_t)2 * k * ORC_NODE;
   int rc = ORC_OK;
 #ifdef _OPENMP
   const int levels = omp_get_max_active_levels();
@@ -421,9 +435,9 @@ int orc_extend_commit_many(const uint8_t* ods, uint32_t n, uint32_t k, size_t sh
 #endif
 #pragma omp parallel reduction(| : rc)
   {
-    uint8_t* eds = (uint8_t*)malloc(eds_b);
-    uint8_t* rr = (uint8_t*)malloc((size_t)2 * k * ORC_NODE);
-    uint8_t* cr = (uint8_t*)malloc((size_t)2 * k * ORC_NODE);
+    uint8_t* eds = thread_scratch(eds_b + 2 * roots_b);
+    uint8_t* rr = eds + eds_b;
+    uint8_t* cr = rr + roots_b;
 #pragma omp for schedule(dynamic, 1)
     for (int64_t i = 0; i < (int64_t)n; i++) {
       int r = orc_extend(ods + (size_t)i * ods_b, k, share, eds);
@@ -431,9 +445,6 @@ int orc_extend_commit_many(const uint8_t* ods, uint32_t n, uint32_t k, size_t sh
       if (r == ORC_OK) orc_dah_hash(rr, cr, 2 * k, dah_out + (size_t)i * 32);
       rc |= r;
     }
-    free(eds);
-    free(rr);
-    free(cr);
   }
 #ifdef _OPENMP
   omp_set_max_active_levels(levels);
@@ -447,16 +458,14 @@ int orc_repair_many(const uint8_t* eds, const uint8_t* present, uint32_t k, size
   const size_t cells = (size_t)4 * k * k, eds_b = cells * share;
 #pragma omp parallel
   {
-    uint8_t* e = (uint8_t*)malloc(eds_b);
-    uint8_t* p = (uint8_t*)malloc(cells);
+    uint8_t* e = thread_scratch(eds_b + cells);
+    uint8_t* p = e + eds_b;
 #pragma omp for schedule(dynamic, 1)
     for (int64_t i = 0; i < (int64_t)n; i++) {
       memcpy(e, eds, eds_b);
       memcpy(p, present, cells);
       status_out[i] = orc_repair(e, p, k, share, row_roots, col_roots, NULL, NULL, NULL, NULL);
     }
-    free(e);
-    free(p);
   }
   return ORC_OK;
 }

@@ -264,7 +264,7 @@ def test_k128_one_corrupt_cell(ctx, oracle, p):
     assert all(s == bs[j].tobytes() for j, s in enumerate(e.Shares) if s is not None)
 
 
-@pytest.mark.parametrize("k", [16, 32, 64, 128])
+@pytest.mark.parametrize("k", [16, 32, 64, 128, 256, 512])
 @pytest.mark.parametrize("in_q1", [True, False])
 def test_sanity_check_bad_encoding(ctx, oracle, k, in_q1):
     """Every cell present, one parity cell changed, and roots computed over that square:
@@ -272,7 +272,9 @@ def test_sanity_check_bad_encoding(ctx, oracle, k, in_q1):
     preRepairSanityCheck catches it (ErrByzantineData with all the axis's shares). Cell
     (3, k+1) breaks row 3 and column k+1, reported as row 3; cell (k+1, 3) breaks row k+1
     and column 3, reported as column 3 (rsmt2d checks row i, then column i). k >= 32:
-    the in-place check kernel in both directions; k = 16: gather -> encode -> compare."""
+    the in-place check kernel in both directions; k = 16: gather -> encode -> compare;
+    k = 256, 512: the GF(2^16) register encoder in check mode, in place on the square (rows
+    at the cell stride, columns at the row stride)."""
     from celestia_eds import _lib
     w = 2 * k
     eds, _, _ = setup(oracle, k, seed=3)
@@ -303,13 +305,13 @@ def test_sanity_check_bad_root(ctx, oracle):
     assert ei.value.status == _lib.EBADROOT and "bad root input" in str(ei.value)
 
 
-def test_orthogonal_completion_then_stuck(ctx, oracle):
+@pytest.mark.parametrize("k", [16, 256])
+def test_orthogonal_completion_then_stuck(ctx, oracle, k):
     """Row r0 decodes and completes column c, whose known cell (r1, c) is corrupted (the
     roots were computed over the corrupted square, so every root matches); nothing else is
     solvable. rsmt2d's check of the newly completed column reports ErrByzantineData(Col, c)
     although the repair is stuck afterwards."""
     from celestia_eds import _lib
-    k = 16
     w = 2 * k
     r0, r1, c = 2, 9, 5
     eds, _, _ = setup(oracle, k, seed=4)
@@ -323,6 +325,27 @@ def test_orthogonal_completion_then_stuck(ctx, oracle):
                                            [x.tobytes() for x in cr])
     assert st == _lib.EBYZANTINE and bad == (1, c)
     assert bp.all() and np.array_equal(bs, eds[:, c])
+
+
+@pytest.mark.parametrize("k", [16, 256])
+def test_solved_axis_bad_encoding(ctx, oracle, k):
+    """An axis that a solve completes, with more than k known cells one of which is
+    corrupted (roots computed over the corrupted square, so no root check can fire first):
+    row 0 holds k + 1 cells, row 1 only k - 1, so rsmt2d's sweep solves row 0 first, and its
+    decode over every known shard is no codeword: verifyEncoding after the solve reports
+    ErrByzantineData(Row, 0). k = 256: the dense GF(2^16) path (gather -> LDS decoder ->
+    encoding check on the dense buffer)."""
+    from celestia_eds import _lib
+    w = 2 * k
+    eds, _, _ = setup(oracle, k, seed=5)
+    eds[0, k + 3, 50] ^= 0x3C
+    _, rr, cr = oracle.roots(eds, check_order=False)
+    present = np.ones((w, w), np.uint8)
+    present[0, :k - 1] = 0
+    present[1, k - 1:] = 0
+    st, bad, _, _ = _assert_same_outcome(ctx, oracle, eds, present, [x.tobytes() for x in rr],
+                                         [x.tobytes() for x in cr])
+    assert st == _lib.EBYZANTINE and bad == (0, 0)
 
 
 def _crossword_passes(present, k):

@@ -83,6 +83,12 @@ def test_extend_shares_errors(ctx):
         da.ExtendShares([bytes(512)] * 5)
     with pytest.raises(CelError):  # 129*129 shares (data_availability_header_test.go:77-80)
         da.ExtendShares([bytes(512)] * (129 * 129))
+    # equal shares of another size: the library's ECHUNK (it never reads past n x 512 B)
+    from celestia_eds import _lib
+    for f in (da.ExtendShares, da.ComputeDataAvailabilityHeader):
+        with pytest.raises(CelError) as ei:
+            f([bytes(256)] * 4)
+        assert ei.value.status == _lib.ECHUNK
 
 
 def test_order_violation_reported(ctx):

@@ -61,3 +61,24 @@ def test_foreign_codec_is_refused():
     assert ei.value.status == _lib.EINVAL
     with pytest.raises(CelError):
         ComputeExtendedDataSquare([bytes(512)], codec=RSGF8Codec())
+
+
+@pytest.mark.parametrize("fn", ["ExtendShares", "ComputeDataAvailabilityHeader"])
+def test_share_inputs_checked_before_the_device(fn):
+    """ExtendShares / ComputeDataAvailabilityHeader hand the C side only n and the share
+    size, so every share must be that size before the buffer is joined: unequal shares get
+    rsmt2d's uneven-chunks error, a non-power-of-two count the reference's ENOTPOW2, and a
+    wrongly shaped array EINVAL, all raised before any device is touched (this runs with no
+    GPU)."""
+    from celestia_eds import CelError, _lib, da
+    f = getattr(da, fn)
+    shares = [bytes(512)] * 3 + [bytes(511)]
+    with pytest.raises(CelError) as ei:
+        f(shares)
+    assert ei.value.status == _lib.ECHUNK and "equal size" in str(ei.value)
+    with pytest.raises(CelError) as ei:
+        f([bytes(512)] * 3)
+    assert ei.value.status == _lib.ENOTPOW2 and "got 3" in str(ei.value)
+    with pytest.raises(CelError) as ei:
+        f(np.zeros((4, 2, 256), np.uint8))
+    assert ei.value.status == _lib.EINVAL

@@ -1,12 +1,22 @@
 #!/bin/bash
-# Build an A/B variant of the library with extra compile flags, outside the product tree:
-#   bash tools/build_variant.sh <name> "<flags>"   ->  variants/lib<name>.so
-# (tools/gpu_variants.sh times variants on the GPU box; variants/ is git-ignored.)
+# Build an A/B variant of the library outside the product tree. The shipped sources carry
+# no A/B knobs: a variant is a patch against celestia-app_amd/csrc (paths as `git diff`
+# prints them) applied to a copy of the sources, plus optional extra compile flags:
+#   bash tools/build_variant.sh <name> [<patch file> | -] ["<flags>"]  ->  variants/lib<name>.so
+# (tools/gpu_variants.sh times variants on the GPU box; build_variants/ and variants/ are
+# git-ignored.)
 set -e
 cd "$(dirname "$0")/.."
-name=$1; flags=$2
+name=$1; patch=${2:--}; flags=$3
 bd=build_variants/$name
-mkdir -p $bd variants
+rm -rf $bd
+mkdir -p $bd/src variants
+cp -r celestia-app_amd/csrc $bd/src/csrc
+cp -r include $bd/include
+if [ "$patch" != "-" ]; then
+  # the patch names celestia-app_amd/csrc/<file>: strip the two leading components
+  (cd $bd/src/csrc && patch -p2 --quiet < "$OLDPWD/$patch")
+fi
 HIPCC=/opt/rocm/bin/hipcc
 srcs="api.cpp square.cpp proof.cpp inclusion.cpp inclusion_paths.cpp rs_kernels.hip rs_bitslice.hip rs_axis.hip rs_decode_axis.hip rs_decode_gf16.hip rs_gf16x.hip nmt_kernels.hip repair_kernels.hip"
 objs=""
@@ -14,7 +24,7 @@ for f in $srcs; do
   extra=""
   [ "$f" = nmt_kernels.hip ] && extra="-mllvm -amdgpu-sched-strategy=max-memory-clause"
   $HIPCC --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result $extra $flags -x hip \
-    -c celestia-app_amd/csrc/$f -o $bd/$f.o &
+    -I$bd/include -c $bd/src/csrc/$f -o $bd/$f.o &
   objs="$objs $bd/$f.o"
 done
 wait

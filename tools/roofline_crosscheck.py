@@ -1,0 +1,110 @@
+"""Cross-check of bench.py's roofline numbers against a rocprofv3 kernel trace of the same
+command (VERDICT r3 ask 4).
+
+The bench times `extend_only` (the RS launch pair) and `commit_only` (the NMT + DAH launches)
+with HIP events on the SquareBatch's launch stream, over B squares at once. In the trace
+those launches are the ones on that stream with the full-batch grids (the timed batch steps
+split B into two chunks on two other streams, so their grids are half the size). This script
+finds the stream of the full-batch rows launch, takes the median duration of every
+(kernel, grid) on it, and rebuilds the line's `roofline.frac` and `roofline_nmt.achieved`.
+
+usage: python tools/roofline_crosscheck.py <trace dir> <bench json> [k] [B]"""
+import collections
+import csv
+import glob
+import json
+import statistics
+import sys
+
+SHA_MEASURED_PEAK = 29.4e9
+# VALU instructions of one SHA-256 compression per wave, from the ISA of the unrolled
+# compression (tools/microbench/sha_rate.hip k_sha_u, tools/isa_mix.py): alignbit, bitop3,
+# add3, VOP2 (add / lshr / xor / mov)
+SHA_ISA = {"v_alignbit_b32": 576, "v_bitop3_b32": 352, "v_add3_u32": 241, "vop2": 134 + 96 + 15}
+
+
+def main():
+    tdir, bjson = sys.argv[1], sys.argv[2]
+    k = int(sys.argv[3]) if len(sys.argv) > 3 else 128
+    B = int(sys.argv[4]) if len(sys.argv) > 4 else 256
+    rows = []
+    for f in glob.glob(tdir + "/**/*kernel_trace.csv", recursive=True):
+        rows += list(csv.DictReader(open(f)))
+    line = None
+    for ln in open(bjson):
+        ln = ln.strip()
+        if ln.startswith("{"):
+            line = json.loads(ln)
+    nslice = 2  # 512-byte shares in 256-byte slices
+    rows_grid = k * nslice * B // 4 * 256  # k_rs_axis_gf8: 4 tiles (waves) per 256-thread workgroup
+    rs_name = "k_rs_axis_gf8"
+    cand = [r for r in rows if rs_name in r["Kernel_Name"] and int(r["Grid_Size_X"]) == rows_grid]
+    if not cand:
+        sys.exit(f"no {rs_name} launch with grid {rows_grid} in {tdir}")
+    rs_kernel = cand[0]["Kernel_Name"]
+    # the chunk streams' column launches have the full-batch rows grid too: the launch stream
+    # is the one that runs the full-batch column launch (grid 2x)
+    colc = [r for r in rows if r["Kernel_Name"] == rs_kernel and int(r["Grid_Size_X"]) == 2 * rows_grid]
+    stream = collections.Counter((r["Stream_Id"], r["Queue_Id"]) for r in colc).most_common(1)[0][0]
+    cand = [r for r in cand if (r["Stream_Id"], r["Queue_Id"]) == stream]
+    # the k-run's window: from its first full-batch rows launch to the first launch of
+    # another RS kernel (the next shape's run: the k=512 line or a rider) after it
+    t0 = min(int(r["Start_Timestamp"]) for r in cand)
+    later = [int(r["Start_Timestamp"]) for r in rows if int(r["Start_Timestamp"]) > t0
+             and ("k_rs" in r["Kernel_Name"] and r["Kernel_Name"] != rs_kernel)]
+    t1 = min(later) if later else float("inf")
+    on = [r for r in rows if (r["Stream_Id"], r["Queue_Id"]) == stream and t0 <= int(r["Start_Timestamp"]) < t1]
+    d = collections.defaultdict(list)
+    for r in on:
+        d[(r["Kernel_Name"], int(r["Grid_Size_X"]))].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    out = []
+    P = out.append
+    P(f"# roofline cross-check: rocprofv3 --kernel-trace of `python3 bench.py` vs its JSON line")
+    P(f"# trace: {tdir}; line: {bjson}; k={k}, B={B}; launch stream {stream[0]} (queue {stream[1]}),")
+    P(f"# the stream of every full-batch RS rows launch (grid {rows_grid}), from the first of them to the next")
+    P(f"# shape's first RS launch ({(t1 - t0) / 1e6 if t1 != float('inf') else 0:.1f} ms); medians over the calls")
+    P(f"{'kernel':70s} {'grid':>10s} {'calls':>5s} {'median_us':>10s}")
+    for (n, g), v in sorted(d.items(), key=lambda x: -statistics.median(x[1])):
+        P(f"{n[:70]:70s} {g:10d} {len(v):5d} {statistics.median(v):10.1f}")
+    rs_rows = statistics.median(d[(rs_kernel, rows_grid)])
+    rs_cols = statistics.median(d[(rs_kernel, 2 * rows_grid)])
+    pair = rs_rows + rs_cols
+    alg = 2048 * k * k * B
+    frac = alg / (pair * 1e-6) / 8e12
+    P("")
+    P(f"RS launch pair (rows {rs_rows:.1f} + cols {rs_cols:.1f}) = {pair:.1f} us; algorithmic 2048 k^2 B = "
+      f"{alg / 1e9:.3f} GB -> {alg / pair / 1e3:.0f} GB/s = frac {frac:.4f} of 8 TB/s")
+    nmt_keys = [(n, g) for (n, g) in d if any(s in n for s in ("k_leaf", "k_level", "k_merkle", "k_dah"))]
+    # commit_only runs every NMT kernel once per call at the full-batch grids on this stream
+    nmt = sum(statistics.median(d[key]) for key in nmt_keys)
+    comp = (60 * k * k + 4 * k - 2) * B
+    P(f"NMT + DAH launches ({len(nmt_keys)} kernels: " + ", ".join(f"{n.split('(')[0][-28:]}@{g}" for n, g in sorted(nmt_keys)) + ")")
+    P(f"  sum of medians {nmt:.1f} us; {comp / 1e6:.1f} M compressions -> {comp / nmt / 1e3:.2f} G/s "
+      f"= {comp / nmt / 1e3 / (SHA_MEASURED_PEAK / 1e9):.3f} of the measured SHA-256 peak")
+    if line:
+        rf, rn = line.get("roofline", {}), line.get("roofline_nmt", {})
+        P("")
+        P(f"bench line: roofline.avg_launch_us {rf.get('avg_launch_us', 0):.1f} (frac {rf.get('frac', 0):.4f}); "
+          f"trace/line pair time {pair / rf.get('avg_launch_us', 1):.3f}")
+        P(f"bench line: roofline_nmt.avg_launch_us {rn.get('avg_launch_us', 0):.1f} (achieved "
+          f"{rn.get('achieved', 0):.2f} G/s); trace/line NMT time {nmt / rn.get('avg_launch_us', 1):.3f} "
+          f"(trace = profiled run)")
+    # SHA-256 ceilings for the NMT phase, three ways
+    n_valu = sum(SHA_ISA.values())
+    guide = 1024 * 2.4e9 * 64 / (2 * n_valu)
+    cyc = 4 * (SHA_ISA["v_alignbit_b32"] + SHA_ISA["v_add3_u32"]) + 2.5 * SHA_ISA["v_bitop3_b32"] + 2 * SHA_ISA["vop2"]
+    model = 1024 * 2.4e9 * 64 / cyc
+    rate = comp / nmt * 1e6
+    P("")
+    P(f"SHA-256 ceilings ({n_valu} VALU per compression per wave: " + ", ".join(f"{k} {v}" for k, v in SHA_ISA.items()) + ")")
+    P(f"  MI355X_MICROARCH.md issue model (every wave64 VALU instruction over 2 cycles, 1024 SIMDs, 2.4 GHz): "
+      f"{guide / 1e9:.1f} G/s -> NMT phase frac {rate / guide:.3f}")
+    P(f"  per-op rates measured here (alignbit / add3 4 cycles, bitop3 2.5, VOP2 2; profiles/r1_microbench_valu.txt): "
+      f"{model / 1e9:.1f} G/s -> frac {rate / model:.3f}")
+    P(f"  the same compression chained in registers, no memory traffic (profiles/r2_sha_rate.txt): "
+      f"{SHA_MEASURED_PEAK / 1e9:.1f} G/s -> frac {rate / SHA_MEASURED_PEAK:.3f}")
+    print("\n".join(out))
+
+
+if __name__ == "__main__":
+    main()
