@@ -185,13 +185,34 @@ cel_status cel_device_name(cel_ctx* ctx, char* buf, size_t len) {
 // tree top + DAH runs beside the other's work. Two chunks (profiles/r1g_pipe_chunks_ab.txt);
 // chaining the extensions so each runs beside the previous chunk's hashing buys nothing,
 // the step is the sum of the two VALU-bound phases (profiles/r2_pipe_overlap_ab.txt).
+// Equal halves: uneven splits (5/8 .. 7/8 of the batch in the first chunk, so the small
+// chunk's tree top would run under the large chunk's bulk) measured slower at both k=64
+// B=128 and k=128 B=256 (profiles/r4_pipe_split_ab.txt).
 constexpr uint32_t kPipeChunks = 2;
 
-static void pipe_plan(uint32_t n, uint32_t* chunk, uint32_t* nchunks) {
-  uint32_t nc = n < kPipeChunks ? n : kPipeChunks;
-  if (nc == 0) nc = 1;
-  *chunk = (n + nc - 1) / nc;
-  *nchunks = (n + *chunk - 1) / *chunk;
+struct PipePlan {
+  uint32_t nchunks;
+  uint32_t first[kPipeChunks], cnt[kPipeChunks];
+  size_t work_off[kPipeChunks], work_bytes;  // NMT workspace of each chunk
+};
+
+static PipePlan pipe_plan(uint32_t k, uint32_t n) {
+  PipePlan p{};
+  uint32_t c0 = n < 2 ? n : (n + 1) / 2;
+  if (c0 >= n) c0 = n;
+  if (c0 == 0) c0 = n;
+  p.nchunks = c0 < n ? 2 : 1;
+  p.first[0] = 0;
+  p.cnt[0] = c0;
+  p.first[1] = c0;
+  p.cnt[1] = n - c0;
+  size_t off = 0;
+  for (uint32_t c = 0; c < p.nchunks; c++) {
+    p.work_off[c] = off;
+    off += (nmt_workspace_size(k, p.cnt[c]) + 255) & ~(size_t)255;
+  }
+  p.work_bytes = off;
+  return p;
 }
 
 // Chunks of the host-buffer pipeline: the upload of chunk c + 1, the compute of chunk c
@@ -208,9 +229,7 @@ void cel_host_free(void* p) {
 }
 
 size_t cel_dev_workspace_size(uint32_t k, uint32_t n) {
-  uint32_t chunk, nchunks;
-  pipe_plan(n, &chunk, &nchunks);
-  const size_t a = nmt_workspace_size(k, n), b = (size_t)nchunks * nmt_workspace_size(k, chunk);
+  const size_t a = nmt_workspace_size(k, n), b = pipe_plan(k, n).work_bytes;
   return a > b ? a : b;
 }
 
@@ -276,14 +295,12 @@ cel_status cel_dev_extend_batch(cel_ctx* ctx, const void* d_ods, uint32_t n, uin
   cel_status st = validate_square(ctx, k, kShare);
   if (st) return st;
   DeviceGuard g(ctx->device);
-  uint32_t chunk, nchunks;
-  pipe_plan(n, &chunk, &nchunks);
-  const size_t ws = nmt_workspace_size(k, chunk);
+  const PipePlan plan = pipe_plan(k, n);
   const uint64_t ods_sq = (uint64_t)k * k * kShare, eds_sq = 4 * ods_sq, roots_sq = (uint64_t)2 * k * kNode;
   hipStream_t us = pick_stream(ctx, stream);
   hipError_t e = hipEventRecord(ctx->ev_start, us);
-  for (uint32_t c = 0; c < nchunks && e == hipSuccess; c++) {
-    const uint32_t first = c * chunk, cnt = (first + chunk <= n) ? chunk : n - first;
+  for (uint32_t c = 0; c < plan.nchunks && e == hipSuccess; c++) {
+    const uint32_t first = plan.first[c], cnt = plan.cnt[c];
     hipStream_t s = ctx->sub[c % cel_ctx::kPipe];
     if ((e = hipStreamWaitEvent(s, ctx->ev_start, 0)) != hipSuccess) break;
     const uint8_t* ods = d_ods ? static_cast<const uint8_t*>(d_ods) + first * ods_sq : nullptr;
@@ -292,7 +309,7 @@ cel_status cel_dev_extend_batch(cel_ctx* ctx, const void* d_ods, uint32_t n, uin
     if ((e = hipEventRecord(ctx->ev_rs[c], s)) != hipSuccess) break;
     e = launch_commit(eds, k, cnt, static_cast<uint8_t*>(d_row_roots) + first * roots_sq,
                       static_cast<uint8_t*>(d_col_roots) + first * roots_sq, static_cast<uint8_t*>(d_dah) + first * 32,
-                      d_status ? d_status + first : nullptr, static_cast<uint8_t*>(d_work) + c * ws,
+                      d_status ? d_status + first : nullptr, static_cast<uint8_t*>(d_work) + plan.work_off[c],
                       (flags & CEL_FLAG_ORDER_CHECK) != 0, s);
     if (e != hipSuccess) break;
     if ((e = hipEventRecord(ctx->ev_done[c], s)) != hipSuccess) break;
