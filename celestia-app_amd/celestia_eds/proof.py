@@ -13,6 +13,11 @@ row_proof.go:12-48) mirrors the reference on the host: nmt VerifyInclusion (nmt
 v0.22.0 proof.go [dep]: leaf hashing with the namespace prefix, completeness check,
 computeRoot) and go-square merkle Proof.Verify (RFC-6962). Host-side hashing is the
 reference's own choice for verifiers (a light client verifies on its CPU).
+
+Wire format (proto/celestia/core/v1/proof/proof.proto:8-49, gogoproto-generated
+pkg/proof/proof.pb.go): ShareProof / RowProof / NMTProof / Proof .Marshal() and
+Unmarshal(bytes), the bytes QueryTxInclusionProof / QueryShareInclusionProof return
+(pkg/proof/querier.go:53-63).
 """
 import ctypes
 import hashlib
@@ -71,6 +76,115 @@ def _rfc_inner(left, right):
     return _sha(b"\x01" + left + right)
 
 
+# ---------------------------------------------------------------- proto3 wire
+# gogoproto's generated Marshal / Unmarshal for these four messages (proof.pb.go):
+# fields in ascending number; scalars and singular bytes omitted when zero / empty;
+# every element of a repeated field written (empty ones too); a set sub-message written
+# even when empty; negative int32 / int64 as 10-byte two's-complement varints. Unmarshal
+# skips unknown fields by wire type and rejects a known field with the wrong wire type.
+def _uvarint(n):
+    n &= (1 << 64) - 1
+    out = bytearray()
+    while True:
+        b = n & 0x7F
+        n >>= 7
+        out.append(b | (0x80 if n else 0))
+        if not n:
+            return bytes(out)
+
+
+def _key(field, wt):
+    return _uvarint(field << 3 | wt)
+
+
+def _w_varint(field, v):
+    return _key(field, 0) + _uvarint(v) if v else b""
+
+
+def _w_bytes(field, b, always=False):
+    b = bytes(b) if b is not None else b""
+    return _key(field, 2) + _uvarint(len(b)) + b if (b or always) else b""
+
+
+class _Reader:
+    def __init__(self, buf, msg):
+        self.buf, self.i, self.msg = bytes(buf), 0, msg
+
+    def _err(self, what):
+        return CelError(_lib.EINVAL, f"proto: {self.msg}: {what}")
+
+    def uvarint(self):
+        v, shift = 0, 0
+        while True:
+            if self.i >= len(self.buf):
+                raise self._err("unexpected EOF")
+            if shift >= 64:
+                raise self._err("integer overflow")
+            b = self.buf[self.i]
+            self.i += 1
+            v |= (b & 0x7F) << shift
+            if not b & 0x80:
+                return v & ((1 << 64) - 1)
+            shift += 7
+
+    def fields(self):
+        """Yield (field number, wire type) until the end; the caller reads the value."""
+        while self.i < len(self.buf):
+            key = self.uvarint()
+            field, wt = key >> 3, key & 7
+            if field <= 0 or key >> 3 > 0x7FFFFFFF:
+                raise self._err(f"illegal tag {field} (wire type {wt})")
+            yield field, wt
+
+    def lendelim(self):
+        n = self.uvarint()
+        if n > len(self.buf) - self.i:
+            raise self._err("unexpected EOF")
+        b = self.buf[self.i:self.i + n]
+        self.i += n
+        return b
+
+    def skip(self, wt, depth=0):
+        if wt == 0:
+            self.uvarint()
+        elif wt == 1:
+            self._need(8)
+        elif wt == 2:
+            self.lendelim()
+        elif wt == 5:
+            self._need(4)
+        elif wt == 3:  # start group: skip to the matching end group
+            if depth > 100:
+                raise self._err("nesting too deep")
+            while True:
+                if self.i >= len(self.buf):
+                    raise self._err("unexpected EOF")
+                key = self.uvarint()
+                if key & 7 == 4:
+                    return
+                self.skip(key & 7, depth + 1)
+        else:  # 4 (end group outside a group), 6, 7
+            raise self._err(f"illegal wireType {wt}")
+
+    def _need(self, n):
+        if n > len(self.buf) - self.i:
+            raise self._err("unexpected EOF")
+        self.i += n
+
+    def want(self, wt, need, name):
+        if wt != need:
+            raise self._err(f"wrong wireType = {wt} for field {name}")
+
+
+def _int32(v):
+    v &= 0xFFFFFFFF
+    return v - (1 << 32) if v >= 1 << 31 else v
+
+
+def _int64(v):
+    return v - (1 << 64) if v >= 1 << 63 else v
+
+
 # -------------------------------------------------------------------- types
 @dataclass
 class NMTProof:
@@ -79,6 +193,32 @@ class NMTProof:
     End: int
     Nodes: List[bytes]
     LeafHash: Optional[bytes] = None
+
+    def Marshal(self):
+        out = _w_varint(1, self.Start) + _w_varint(2, self.End)
+        for n in self.Nodes:
+            out += _w_bytes(3, n, always=True)
+        return out + _w_bytes(4, self.LeafHash)
+
+    @classmethod
+    def Unmarshal(cls, buf):
+        m, r = cls(0, 0, []), _Reader(buf, "NMTProof")
+        for f, wt in r.fields():
+            if f == 1:
+                r.want(wt, 0, "Start")
+                m.Start = _int32(r.uvarint())
+            elif f == 2:
+                r.want(wt, 0, "End")
+                m.End = _int32(r.uvarint())
+            elif f == 3:
+                r.want(wt, 2, "Nodes")
+                m.Nodes.append(r.lendelim())
+            elif f == 4:
+                r.want(wt, 2, "LeafHash")
+                m.LeafHash = r.lendelim()
+            else:
+                r.skip(wt)
+        return m
 
     def VerifyInclusion(self, namespace, leaves, root):
         """nmt Proof.VerifyInclusion: recompute the root from the leaves (all in `namespace`,
@@ -131,6 +271,32 @@ class Proof:
     LeafHash: bytes
     Aunts: List[bytes]
 
+    def Marshal(self):
+        out = _w_varint(1, self.Total) + _w_varint(2, self.Index) + _w_bytes(3, self.LeafHash)
+        for a in self.Aunts:
+            out += _w_bytes(4, a, always=True)
+        return out
+
+    @classmethod
+    def Unmarshal(cls, buf):
+        m, r = cls(0, 0, b"", []), _Reader(buf, "Proof")
+        for f, wt in r.fields():
+            if f == 1:
+                r.want(wt, 0, "Total")
+                m.Total = _int64(r.uvarint())
+            elif f == 2:
+                r.want(wt, 0, "Index")
+                m.Index = _int64(r.uvarint())
+            elif f == 3:
+                r.want(wt, 2, "LeafHash")
+                m.LeafHash = r.lendelim()
+            elif f == 4:
+                r.want(wt, 2, "Aunts")
+                m.Aunts.append(r.lendelim())
+            else:
+                r.skip(wt)
+        return m
+
     def _compute(self, index, total, leaf, aunts):
         if total == 1:
             return leaf if not aunts else None
@@ -159,6 +325,36 @@ class RowProof:
     Proofs: List[Proof]
     StartRow: int
     EndRow: int
+    Root: bytes = b""  # proof.proto field 3; NewShareInclusionProofFromEDS leaves it empty
+
+    def Marshal(self):
+        out = b"".join(_w_bytes(1, r, always=True) for r in self.RowRoots)
+        for p in self.Proofs:
+            out += _w_bytes(2, p.Marshal(), always=True)
+        return out + _w_bytes(3, self.Root) + _w_varint(4, self.StartRow) + _w_varint(5, self.EndRow)
+
+    @classmethod
+    def Unmarshal(cls, buf):
+        m, r = cls([], [], 0, 0), _Reader(buf, "RowProof")
+        for f, wt in r.fields():
+            if f == 1:
+                r.want(wt, 2, "RowRoots")
+                m.RowRoots.append(r.lendelim())
+            elif f == 2:
+                r.want(wt, 2, "Proofs")
+                m.Proofs.append(Proof.Unmarshal(r.lendelim()))
+            elif f == 3:
+                r.want(wt, 2, "Root")
+                m.Root = r.lendelim()
+            elif f == 4:
+                r.want(wt, 0, "StartRow")
+                m.StartRow = r.uvarint() & 0xFFFFFFFF
+            elif f == 5:
+                r.want(wt, 0, "EndRow")
+                m.EndRow = r.uvarint() & 0xFFFFFFFF
+            else:
+                r.skip(wt)
+        return m
 
     def Validate(self, root):
         if self.EndRow - self.StartRow + 1 != len(self.RowRoots):
@@ -184,10 +380,45 @@ class ShareProof:
     Data: List[bytes]
     ShareProofs: List[NMTProof]
     NamespaceId: bytes
-    RowProof: RowProof
+    RowProof: Optional[RowProof]
     NamespaceVersion: int = 0
 
+    def Marshal(self):
+        """gogoproto ShareProof.Marshal (proof.pb.go): the bytes of the ABCI proof queries."""
+        out = b"".join(_w_bytes(1, d, always=True) for d in self.Data)
+        for p in self.ShareProofs:
+            out += _w_bytes(2, p.Marshal(), always=True)
+        out += _w_bytes(3, self.NamespaceId)
+        if self.RowProof is not None:
+            out += _w_bytes(4, self.RowProof.Marshal(), always=True)
+        return out + _w_varint(5, self.NamespaceVersion)
+
+    @classmethod
+    def Unmarshal(cls, buf):
+        m, r = cls([], [], b"", None), _Reader(buf, "ShareProof")
+        for f, wt in r.fields():
+            if f == 1:
+                r.want(wt, 2, "Data")
+                m.Data.append(r.lendelim())
+            elif f == 2:
+                r.want(wt, 2, "ShareProofs")
+                m.ShareProofs.append(NMTProof.Unmarshal(r.lendelim()))
+            elif f == 3:
+                r.want(wt, 2, "NamespaceId")
+                m.NamespaceId = r.lendelim()
+            elif f == 4:
+                r.want(wt, 2, "RowProof")
+                m.RowProof = RowProof.Unmarshal(r.lendelim())
+            elif f == 5:
+                r.want(wt, 0, "NamespaceVersion")
+                m.NamespaceVersion = r.uvarint() & 0xFFFFFFFF
+            else:
+                r.skip(wt)
+        return m
+
     def Validate(self, root):
+        if self.RowProof is None:  # the reference dereferences a nil *RowProof (a panic)
+            raise CelError(_lib.EINVAL, "share proof has no row proof")
         if not self.Data:
             raise CelError(_lib.EINVAL, "empty share proof")
         n = sum(p.End - p.Start for p in self.ShareProofs)
