@@ -89,6 +89,9 @@ def parse():
                     help="eds: the upload places each ODS in Q0 of its EDS buffer and the extension "
                          "reads it in place; ods: separate contiguous ODS buffer, the row pass copies Q0")
     ap.add_argument("--phase-reps", type=int, default=10)
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="batches in flight: steps go round-robin over this many batches, each with its own "
+                         "buffers and stream (independent blocks back to back)")
     ap.add_argument("--k512-batch", type=int, default=32,
                     help="with --k 128: k=512 squares per step per GPU of the companion line (0 = off)")
     ap.add_argument("--k512-steps", type=int, default=5)
@@ -733,33 +736,43 @@ def measure_rowshard(k, world, rank, local, dist, dev, steps, warmup, barrier, d
     return f
 
 
-def _measure_batch(ctx, local, rank, k, B, steps, warmup, n_distinct, layout, phase_reps, barrier, dist, dev):
+def _measure_batch(ctx, local, rank, k, B, steps, warmup, n_distinct, layout, phase_reps, barrier, dist, dev,
+                   inflight=1):
     """Time `steps` batch steps of B k x k squares resident in HBM (barrier + synchronize
     on both sides, max over ranks), then the RS and NMT phases alone with HIP events on
-    the batch's launch stream."""
+    the batch's launch stream. inflight > 1: that many batches (own buffers and caller
+    stream each) take the steps in turn, so one step's latency-bound tree tops and DAH run
+    beside the next step's bulk (independent blocks replayed back to back); every step
+    still extends and commits all B squares."""
     from celestia_eds.device import SquareBatch
     from celestia_eds.testfactory import random_ods
 
-    sb = SquareBatch(B, k, device=local, ctx=ctx, ods_in_eds=(layout == "eds"))
+    sbs = []
     distinct = [random_ods(k, 1_000_003 * rank + i) for i in range(min(n_distinct, B))]
-    host = np.stack([distinct[i % len(distinct)] for i in range(B)])
-    sb.load_ods(torch.from_numpy(host))
-    del host
+    for j in range(max(1, inflight)):
+        sb = SquareBatch(B, k, device=local, ctx=ctx, ods_in_eds=(layout == "eds"))
+        host = np.stack([distinct[(i + j) % len(distinct)] for i in range(B)])
+        sb.load_ods(torch.from_numpy(host))
+        del host
+        sbs.append(sb)
     torch.cuda.synchronize()
-    for _ in range(warmup):
-        sb.extend_and_commit()
+    for i in range(warmup):
+        sbs[i % len(sbs)].extend_and_commit()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        sb.extend_and_commit()
+    for i in range(steps):
+        sbs[i % len(sbs)].extend_and_commit()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     elapsed = _max_over_ranks(time.perf_counter() - t0, dist, dev)
-    status = sb.status.cpu().numpy()
-    assert (status == 0).all(), f"device reported status {status}"
+    for sb in sbs:
+        status = sb.status.cpu().numpy()
+        assert (status == 0).all(), f"device reported status {status}"
+    sb = sbs[0]
+    del sbs
 
     stream = sb.hip_stream  # the stream every launch of `sb` goes to
 
@@ -877,7 +890,7 @@ def main():
             dist.barrier()
 
     m = _measure_batch(ctx, local, rank, a.k, a.batch, a.steps, a.warmup, a.distinct, a.input,
-                       a.phase_reps, barrier, dist, dev)
+                       a.phase_reps, barrier, dist, dev, a.inflight)
     k, B, elapsed, t_ext, t_com = a.k, a.batch, m["elapsed"], m["t_ext"], m["t_com"]
     sb, distinct = m["sb"], m["distinct"]
     del m

@@ -339,3 +339,46 @@ def test_batch_parity_only(ctx, oracle, k, n):
         assert (eds[i, :k, :k] == 0xA5).all(), f"square {i}: Q0 was written"
         assert np.array_equal(eds[i, :k, k:], e[:k, k:]) and np.array_equal(eds[i, k:], e[k:]), f"square {i}: parity"
         assert np.array_equal(rr[i], r) and np.array_equal(cr[i], c) and dah[i].tobytes() == d
+
+
+@pytest.mark.parametrize("k,n", [(32, 3), (64, 4)])
+def test_batches_in_flight_on_two_streams(ctx, oracle, k, n):
+    """Independent batches issued back to back on two caller streams (bench --inflight 2):
+    consecutive cel_dev_extend_batch calls take alternate internal stream pairs, so the
+    batches overlap on the device. Each batch's buffers are rewritten by every one of its
+    calls; after six alternating calls (and again after a reload of one batch between
+    calls) every EDS, root and DAH equals the oracle's."""
+    import torch
+    from celestia_eds.device import SquareBatch
+    a = SquareBatch(n, k, device=0, ctx=ctx, ods_in_eds=True)
+    b = SquareBatch(n, k, device=0, ctx=ctx, ods_in_eds=True)
+    oa = np.stack([random_ods(k, 7100 + i) for i in range(n)])
+    ob = np.stack([random_ods(k, 7200 + i) for i in range(n)])
+    a.load_ods(torch.from_numpy(oa))
+    b.load_ods(torch.from_numpy(ob))
+    torch.cuda.synchronize()
+    for _ in range(3):
+        a.extend_and_commit()
+        b.extend_and_commit()
+
+    def check(sb, odss):
+        torch.cuda.synchronize()
+        eds, rr, cr = sb.eds.cpu().numpy(), sb.row_roots.cpu().numpy(), sb.col_roots.cpu().numpy()
+        dah, st = sb.dah.cpu().numpy(), sb.status.cpu().numpy()
+        assert (st == 0).all()
+        for i in range(n):
+            e, r, c, d = oracle.extend_and_commit(odss[i])
+            assert np.array_equal(eds[i], e) and np.array_equal(rr[i], r) and np.array_equal(cr[i], c)
+            assert dah[i].tobytes() == d
+
+    check(a, oa)
+    check(b, ob)
+    # a's stream reloads its input while b's batch may still run: the batches stay independent
+    b.extend_and_commit()
+    oa2 = np.stack([random_ods(k, 7300 + i) for i in range(n)])
+    with torch.cuda.stream(a.hip_stream):
+        a.load_ods(torch.from_numpy(oa2))
+    a.extend_and_commit()
+    b.extend_and_commit()
+    check(a, oa2)
+    check(b, ob)

@@ -14,8 +14,8 @@ mkdir -p $bd/src variants
 cp -r celestia-app_amd/csrc $bd/src/csrc
 cp -r include $bd/include
 if [ "$patch" != "-" ]; then
-  # the patch names celestia-app_amd/csrc/<file>: strip the two leading components
-  (cd $bd/src/csrc && patch -p2 --quiet < "$OLDPWD/$patch")
+  # the patch names a/celestia-app_amd/csrc/<file> (git diff form): strip two components
+  (cd $bd/src && patch -p2 --quiet < "$OLDPWD/$patch")
 fi
 HIPCC=/opt/rocm/bin/hipcc
 srcs="api.cpp square.cpp proof.cpp inclusion.cpp inclusion_paths.cpp rs_kernels.hip rs_bitslice.hip rs_axis.hip rs_decode_axis.hip rs_decode_gf16.hip rs_gf16x.hip nmt_kernels.hip repair_kernels.hip"

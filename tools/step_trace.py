@@ -5,7 +5,9 @@
   python3 tools/timeline.py <dir> 1000 -2
 
 Each step is cel_dev_extend_batch over B resident squares (as bench.py's timed steps),
-followed by a synchronize and a 3 ms sleep so the trace splits into one burst per step."""
+followed by a synchronize and a 3 ms sleep so the trace splits into one burst per step.
+--inflight M: a burst is M steps issued back to back on M batches (own buffers and
+stream each), as bench.py --inflight M times them."""
 import argparse
 import os
 import sys
@@ -20,16 +22,23 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--k", type=int, default=64)
 ap.add_argument("--batch", type=int, default=128)
 ap.add_argument("--steps", type=int, default=4)
+ap.add_argument("--inflight", type=int, default=1)
 a = ap.parse_args()
 from celestia_eds.device import SquareBatch  # noqa: E402
 from celestia_eds.testfactory import random_ods  # noqa: E402
 
-sb = SquareBatch(a.batch, a.k, ods_in_eds=True)
-sb.load_ods(torch.from_numpy(np.stack([random_ods(a.k, 3 + (i % 4)) for i in range(a.batch)])))
+sbs = []
+for j in range(max(1, a.inflight)):
+    sb = SquareBatch(a.batch, a.k, ods_in_eds=True)
+    sb.load_ods(torch.from_numpy(np.stack([random_ods(a.k, 3 + ((i + j) % 4)) for i in range(a.batch)])))
+    sbs.append(sb)
 for i in range(a.steps):
     t0 = time.perf_counter()
-    sb.extend_and_commit()
+    for sb in sbs:
+        sb.extend_and_commit()
     torch.cuda.synchronize()
-    print(f"step {i}: {(time.perf_counter() - t0) * 1e3:.3f} ms (host, synchronized)", flush=True)
+    print(f"burst {i}: {(time.perf_counter() - t0) * 1e3:.3f} ms for {len(sbs)} step(s) (host, synchronized)",
+          flush=True)
     time.sleep(0.003)
-assert (sb.status.cpu().numpy() == 0).all()
+for sb in sbs:
+    assert (sb.status.cpu().numpy() == 0).all()
