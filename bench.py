@@ -740,30 +740,33 @@ def _measure_batch(ctx, local, rank, k, B, steps, warmup, n_distinct, layout, ph
                    inflight=1):
     """Time `steps` batch steps of B k x k squares resident in HBM (barrier + synchronize
     on both sides, max over ranks), then the RS and NMT phases alone with HIP events on
-    the batch's launch stream. inflight > 1: that many batches (own buffers and caller
-    stream each) take the steps in turn, so one step's latency-bound tree tops and DAH run
-    beside the next step's bulk (independent blocks replayed back to back); every step
-    still extends and commits all B squares."""
+    the batch's launch stream. inflight > 1: that many batches (own buffers and stream
+    each) take the steps in turn, each step as one chunk on its batch's stream
+    (CEL_FLAG_CALLER_STREAM), so one step's latency-bound tree tops and DAH run beside the
+    next step's bulk (independent blocks replayed back to back); every step still extends
+    and commits all B squares."""
     from celestia_eds.device import SquareBatch
     from celestia_eds.testfactory import random_ods
 
     sbs = []
     distinct = [random_ods(k, 1_000_003 * rank + i) for i in range(min(n_distinct, B))]
     for j in range(max(1, inflight)):
-        sb = SquareBatch(B, k, device=local, ctx=ctx, ods_in_eds=(layout == "eds"))
+        prio = -1 if (j == 0 and inflight > 1 and os.environ.get("CEL_BENCH_PRIO") == "1") else 0
+        sb = SquareBatch(B, k, device=local, ctx=ctx, ods_in_eds=(layout == "eds"), priority=prio)
         host = np.stack([distinct[(i + j) % len(distinct)] for i in range(B)])
         sb.load_ods(torch.from_numpy(host))
         del host
         sbs.append(sb)
     torch.cuda.synchronize()
+    piped = len(sbs) > 1
     for i in range(warmup):
-        sbs[i % len(sbs)].extend_and_commit()
+        sbs[i % len(sbs)].extend_and_commit(caller_stream=piped)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(steps):
-        sbs[i % len(sbs)].extend_and_commit()
+        sbs[i % len(sbs)].extend_and_commit(caller_stream=piped)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()

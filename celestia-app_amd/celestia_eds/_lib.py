@@ -17,6 +17,7 @@ OK, EINVAL, ENOTPOW2, ECHUNK, ETOOBIG, EORDER, ETOOFEW, EBYZANTINE, EUNREPAIRABL
     ESHORT, EPUSHPAST, EBADROOT, ENODATA = range(15)
 FLAG_ORDER_CHECK = 0x1
 FLAG_PARITY_ONLY = 0x2
+FLAG_CALLER_STREAM = 0x4
 SHARE_SIZE = 512
 NAMESPACE_SIZE = 29
 NMT_NODE_SIZE = 90

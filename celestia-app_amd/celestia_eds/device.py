@@ -22,7 +22,7 @@ class SquareBatch:
     place (d_ods = NULL in the C ABI): no separate ODS buffer and no Q0 copy pass.
     """
 
-    def __init__(self, n, k, device=0, ctx=None, ods_in_eds=False):
+    def __init__(self, n, k, device=0, ctx=None, ods_in_eds=False, priority=0):
         import torch
         self.torch = torch
         self.n, self.k = n, k
@@ -42,7 +42,7 @@ class SquareBatch:
         self.work = torch.empty((ws,), dtype=torch.uint8, device=self.dev)
         # A dedicated (non-null) stream: every launch of this batch goes there, and
         # callers time it with events recorded on self.hip_stream.
-        self.hip_stream = torch.cuda.Stream(device=self.dev)
+        self.hip_stream = torch.cuda.Stream(device=self.dev, priority=priority)
 
     def load_ods(self, host):
         """Upload [n][k][k][512] host shares (uint8 array or tensor) into the ODS input."""
@@ -55,12 +55,14 @@ class SquareBatch:
     def stream(self):
         return ctypes.c_void_p(self.hip_stream.cuda_stream)
 
-    def extend_and_commit(self, order_check=True):
+    def extend_and_commit(self, order_check=True, caller_stream=False):
+        """caller_stream: the whole batch on self.hip_stream (CEL_FLAG_CALLER_STREAM), for
+        callers that keep several batches in flight on their own streams."""
         c = self.ctx
+        flags = (_lib.FLAG_ORDER_CHECK if order_check else 0) | (_lib.FLAG_CALLER_STREAM if caller_stream else 0)
         c.check(c.lib.cel_dev_extend_batch(c.handle, self._ods_arg(), self.n, self.k, _ptr(self.eds),
                                            _ptr(self.row_roots), _ptr(self.col_roots), _ptr(self.dah),
-                                           _ptr(self.status), _ptr(self.work), self.stream(),
-                                           _lib.FLAG_ORDER_CHECK if order_check else 0))
+                                           _ptr(self.status), _ptr(self.work), self.stream(), flags))
 
     def extend_only(self):
         c = self.ctx

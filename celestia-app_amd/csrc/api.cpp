@@ -100,7 +100,6 @@ cel_status cel_ctx_create(int device, cel_ctx** out) {
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_rs[i], hipEventDisableTiming);
   }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_start, hipEventDisableTiming);
-  for (int i = 0; i < 2 && e == hipSuccess; i++) e = hipEventCreateWithFlags(&ctx->ev_turn[i], hipEventDisableTiming);
   for (int i = 0; i < cel_ctx::kPipe && e == hipSuccess; i++) {
     e = hipEventCreateWithFlags(&ctx->ev_dl[i], hipEventDisableTiming);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->dl[i], hipStreamNonBlocking);
@@ -130,8 +129,6 @@ void cel_ctx_destroy(cel_ctx* ctx) {
       if (ctx->ev_rs[i]) (void)hipEventDestroy(ctx->ev_rs[i]);
     }
     if (ctx->ev_start) (void)hipEventDestroy(ctx->ev_start);
-    for (int i = 0; i < 2; i++)
-      if (ctx->ev_turn[i]) (void)hipEventDestroy(ctx->ev_turn[i]);
     for (int i = 0; i < cel_ctx::kPipe; i++) {
       if (ctx->dl[i]) {
         (void)hipStreamSynchronize(ctx->dl[i]);
@@ -192,7 +189,6 @@ cel_status cel_device_name(cel_ctx* ctx, char* buf, size_t len) {
 // chunk's tree top would run under the large chunk's bulk) measured slower at both k=64
 // B=128 and k=128 B=256 (profiles/r4_pipe_split_ab.txt).
 constexpr uint32_t kPipeChunks = 2;
-static_assert(2 * kPipeChunks <= cel_ctx::kPipe, "two stream pairs for calls in flight");
 
 struct PipePlan {
   uint32_t nchunks;
@@ -302,17 +298,24 @@ cel_status cel_dev_extend_batch(cel_ctx* ctx, const void* d_ods, uint32_t n, uin
   const PipePlan plan = pipe_plan(k, n);
   const uint64_t ods_sq = (uint64_t)k * k * kShare, eds_sq = 4 * ods_sq, roots_sq = (uint64_t)2 * k * kNode;
   hipStream_t us = pick_stream(ctx, stream);
-  // Consecutive calls alternate between the two pairs of internal streams: a batch issued
-  // on another caller stream than the previous one then does not queue behind that
-  // batch's latency-bound tree tops and DAH, which run beside its bulk instead
-  // (profiles/r4_inflight_ab.txt). Calls on one caller stream stay ordered by the join.
-  const uint32_t base = (ctx->pipe_turn++ & 1u) * kPipeChunks;
-  hipEvent_t go = ctx->ev_turn[base / kPipeChunks];
-  hipError_t e = hipEventRecord(go, us);
+  if (flags & CEL_FLAG_CALLER_STREAM) {
+    // One chunk on the caller's stream: a caller with several batches in flight on its
+    // own streams overlaps one batch's latency-bound tree tops and DAH with the next
+    // one's bulk itself (profiles/r4_inflight_ab.txt). No internal streams are touched,
+    // so the batches do not meet on shared hardware queues.
+    hipError_t e = launch_extend(static_cast<const uint8_t*>(d_ods), static_cast<uint8_t*>(d_eds), k, n,
+                                 ctx->tables, us);
+    if (e == hipSuccess)
+      e = launch_commit(static_cast<const uint8_t*>(d_eds), k, n, static_cast<uint8_t*>(d_row_roots),
+                        static_cast<uint8_t*>(d_col_roots), static_cast<uint8_t*>(d_dah), d_status, d_work,
+                        (flags & CEL_FLAG_ORDER_CHECK) != 0, us);
+    return e == hipSuccess ? CEL_OK : hip_fail(ctx, e, "extend batch");
+  }
+  hipError_t e = hipEventRecord(ctx->ev_start, us);
   for (uint32_t c = 0; c < plan.nchunks && e == hipSuccess; c++) {
     const uint32_t first = plan.first[c], cnt = plan.cnt[c];
-    hipStream_t s = ctx->sub[base + c];
-    if ((e = hipStreamWaitEvent(s, go, 0)) != hipSuccess) break;
+    hipStream_t s = ctx->sub[c % cel_ctx::kPipe];
+    if ((e = hipStreamWaitEvent(s, ctx->ev_start, 0)) != hipSuccess) break;
     const uint8_t* ods = d_ods ? static_cast<const uint8_t*>(d_ods) + first * ods_sq : nullptr;
     uint8_t* eds = static_cast<uint8_t*>(d_eds) + first * eds_sq;
     if ((e = launch_extend(ods, eds, k, cnt, ctx->tables, s)) != hipSuccess) break;
@@ -321,8 +324,8 @@ cel_status cel_dev_extend_batch(cel_ctx* ctx, const void* d_ods, uint32_t n, uin
                       d_status ? d_status + first : nullptr, static_cast<uint8_t*>(d_work) + plan.work_off[c],
                       (flags & CEL_FLAG_ORDER_CHECK) != 0, s);
     if (e != hipSuccess) break;
-    if ((e = hipEventRecord(ctx->ev_done[base + c], s)) != hipSuccess) break;
-    e = hipStreamWaitEvent(us, ctx->ev_done[base + c], 0);
+    if ((e = hipEventRecord(ctx->ev_done[c], s)) != hipSuccess) break;
+    e = hipStreamWaitEvent(us, ctx->ev_done[c], 0);
   }
   return e == hipSuccess ? CEL_OK : hip_fail(ctx, e, "extend batch");
 }

@@ -201,9 +201,6 @@ struct cel_ctx {
   hipStream_t stream = nullptr;
   hipStream_t sub[kPipe] = {nullptr, nullptr, nullptr, nullptr};
   hipEvent_t ev_start = nullptr;
-  // cel_dev_extend_batch: calls alternate between stream pairs sub[0..1] and sub[2..3]
-  uint32_t pipe_turn = 0;
-  hipEvent_t ev_turn[2] = {};
   hipEvent_t ev_done[kChunks] = {};
   hipEvent_t ev_rs[kChunks] = {};
   // EDS downloads of the host pipeline, one per pipeline stream (beside the hashing)

@@ -61,6 +61,9 @@ typedef int32_t cel_status;
                                        (Q1, Q2, Q3); its Q0 cells are not written, the caller
                                        holds the ODS already (the Go shim points Q0's cells of the
                                        imported square at the input shares): 3/4 of the PCIe bytes */
+#define CEL_FLAG_CALLER_STREAM 0x4u /* cel_dev_extend_batch: the whole batch as one chunk on the
+                                       caller's stream, no internal streams (a caller keeping
+                                       several batches in flight on its own streams) */
 
 #define CEL_SHARE_SIZE 512u
 #define CEL_NAMESPACE_SIZE 29u

@@ -18,6 +18,11 @@ def hip():
         _hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
         _hip.hipMemset.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t]
         _hip.hipDeviceSynchronize.argtypes = []
+        _hip.hipStreamCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+        _hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+        _hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+        _hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                        ctypes.c_void_p]
     return _hip
 
 
@@ -41,6 +46,15 @@ class DeviceBuffer:
         assert a.nbytes <= self.nbytes
         _ck(hip().hipMemcpy(self.ptr, a.ctypes.data_as(ctypes.c_void_p), a.nbytes, _H2D), "H2D")
 
+    def upload_async(self, arr, stream):
+        """H2D on `stream` (ordered after the stream's earlier work); `arr` must stay alive
+        until the stream is synchronized."""
+        a = np.ascontiguousarray(arr)
+        assert a.nbytes <= self.nbytes
+        _ck(hip().hipMemcpyAsync(self.ptr, a.ctypes.data_as(ctypes.c_void_p), a.nbytes, _H2D, stream.ptr),
+            "H2D async")
+        return a
+
     def download(self, shape, dtype=np.uint8):
         out = np.empty(shape, dtype)
         assert out.nbytes <= self.nbytes
@@ -55,6 +69,22 @@ class DeviceBuffer:
     def __del__(self):
         try:
             self.free()
+        except Exception:
+            pass
+
+
+class Stream:
+    def __init__(self):
+        self.ptr = ctypes.c_void_p()
+        _ck(hip().hipStreamCreate(ctypes.byref(self.ptr)), "hipStreamCreate")
+
+    def synchronize(self):
+        _ck(hip().hipStreamSynchronize(self.ptr), "hipStreamSynchronize")
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                hip().hipStreamDestroy(self.ptr)
         except Exception:
             pass
 

@@ -344,41 +344,60 @@ def test_batch_parity_only(ctx, oracle, k, n):
 @pytest.mark.parametrize("k,n", [(32, 3), (64, 4)])
 def test_batches_in_flight_on_two_streams(ctx, oracle, k, n):
     """Independent batches issued back to back on two caller streams (bench --inflight 2):
-    consecutive cel_dev_extend_batch calls take alternate internal stream pairs, so the
-    batches overlap on the device. Each batch's buffers are rewritten by every one of its
-    calls; after six alternating calls (and again after a reload of one batch between
-    calls) every EDS, root and DAH equals the oracle's."""
-    import torch
-    from celestia_eds.device import SquareBatch
-    a = SquareBatch(n, k, device=0, ctx=ctx, ods_in_eds=True)
-    b = SquareBatch(n, k, device=0, ctx=ctx, ods_in_eds=True)
-    oa = np.stack([random_ods(k, 7100 + i) for i in range(n)])
-    ob = np.stack([random_ods(k, 7200 + i) for i in range(n)])
-    a.load_ods(torch.from_numpy(oa))
-    b.load_ods(torch.from_numpy(ob))
-    torch.cuda.synchronize()
+    with CEL_FLAG_CALLER_STREAM each batch runs as one chunk on its caller's stream, so the
+    batches overlap on the device; a third batch on the internal two-chunk pipeline runs
+    beside them. Each batch's buffers are rewritten by every one of its calls; after
+    alternating calls, and again after one batch's input is reloaded on its own stream
+    between calls, every EDS, root and DAH equals the oracle's."""
+    import ctypes
+    from celestia_eds import _lib
+    from hipmem import DeviceBuffer, Stream, synchronize
+    w = 2 * k
+
+    class Batch:
+        def __init__(self, seed, flags):
+            self.s, self.flags = Stream(), flags
+            self.eds = DeviceBuffer(n * w * w * 512, fill=0)
+            self.rr, self.cr = DeviceBuffer(n * w * 90), DeviceBuffer(n * w * 90)
+            self.dah, self.st = DeviceBuffer(n * 32), DeviceBuffer(n * 4, fill=0x7F)
+            self.work = DeviceBuffer(ctx.lib.cel_dev_workspace_size(k, n))
+            self.load(seed)
+
+        def load(self, seed):
+            self.odss = np.stack([random_ods(k, seed + i) for i in range(n)])
+            ctx.check(ctx.lib.cel_dev_place_ods(ctx.handle, self.odss.ctypes.data_as(ctypes.c_void_p), n, k,
+                                                self.eds.ptr, self.s.ptr))
+
+        def step(self):
+            ctx.check(ctx.lib.cel_dev_extend_batch(ctx.handle, None, n, k, self.eds.ptr, self.rr.ptr, self.cr.ptr,
+                                                   self.dah.ptr, self.st.ptr, self.work.ptr, self.s.ptr,
+                                                   _lib.FLAG_ORDER_CHECK | self.flags))
+
+        def check(self):
+            self.s.synchronize()
+            eds = self.eds.download((n, w, w, 512))
+            rr, cr = self.rr.download((n, w, 90)), self.cr.download((n, w, 90))
+            dah, st = self.dah.download((n, 32)), self.st.download((n,), np.int32)
+            assert (st == 0).all()
+            for i in range(n):
+                e, r, c, d = oracle.extend_and_commit(self.odss[i])
+                assert np.array_equal(eds[i], e) and np.array_equal(rr[i], r) and np.array_equal(cr[i], c)
+                assert dah[i].tobytes() == d
+
+    a, b = Batch(7100, _lib.FLAG_CALLER_STREAM), Batch(7200, _lib.FLAG_CALLER_STREAM)
+    c = Batch(7400, 0)
     for _ in range(3):
-        a.extend_and_commit()
-        b.extend_and_commit()
-
-    def check(sb, odss):
-        torch.cuda.synchronize()
-        eds, rr, cr = sb.eds.cpu().numpy(), sb.row_roots.cpu().numpy(), sb.col_roots.cpu().numpy()
-        dah, st = sb.dah.cpu().numpy(), sb.status.cpu().numpy()
-        assert (st == 0).all()
-        for i in range(n):
-            e, r, c, d = oracle.extend_and_commit(odss[i])
-            assert np.array_equal(eds[i], e) and np.array_equal(rr[i], r) and np.array_equal(cr[i], c)
-            assert dah[i].tobytes() == d
-
-    check(a, oa)
-    check(b, ob)
-    # a's stream reloads its input while b's batch may still run: the batches stay independent
-    b.extend_and_commit()
-    oa2 = np.stack([random_ods(k, 7300 + i) for i in range(n)])
-    with torch.cuda.stream(a.hip_stream):
-        a.load_ods(torch.from_numpy(oa2))
-    a.extend_and_commit()
-    b.extend_and_commit()
-    check(a, oa2)
-    check(b, ob)
+        a.step()
+        b.step()
+        c.step()
+    a.check()
+    b.check()
+    c.check()
+    # a's input is reloaded on a's stream while b's batch may still run
+    b.step()
+    a.load(7300)
+    a.step()
+    b.step()
+    a.check()
+    b.check()
+    synchronize()

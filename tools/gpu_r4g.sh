@@ -14,7 +14,7 @@ out=gpurun_out/${tag}_inflight_ab.txt
 for rep in 1 2; do
   for cfg in "64 128" "64 1024" "128 256"; do
     set -- $cfg
-    for inf in 1 2; do
+    for inf in 1 2 3; do
       timeout -k 10 180 python bench.py --k $1 --batch $2 --steps 20 --warmup 3 --inflight $inf --no-cpu --no-riders \
         --k512-batch 0 --no-host-io > gpurun_out/${tag}_b.json 2> gpurun_out/${tag}_b.err || { cat gpurun_out/${tag}_b.err; exit 2; }
       python - "$1" "$2" "$inf" gpurun_out/${tag}_b.json >> $out <<'PY'
@@ -29,4 +29,4 @@ done
 cat $out
 timeout -k 10 240 rocprofv3 --kernel-trace -d gpurun_out/${tag}_trace -o tr -- python3 tools/step_trace.py --k 64 --batch 128 \
   --inflight 2 > gpurun_out/${tag}_trace.log 2>&1 || { tail -20 gpurun_out/${tag}_trace.log; exit 3; }
-echo trace ok
+python3 tools/timeline.py gpurun_out/${tag}_trace 1000 -2 > gpurun_out/${tag}_timeline.txt && tail -25 gpurun_out/${tag}_timeline.txt

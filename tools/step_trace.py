@@ -35,7 +35,7 @@ for j in range(max(1, a.inflight)):
 for i in range(a.steps):
     t0 = time.perf_counter()
     for sb in sbs:
-        sb.extend_and_commit()
+        sb.extend_and_commit(caller_stream=len(sbs) > 1)
     torch.cuda.synchronize()
     print(f"burst {i}: {(time.perf_counter() - t0) * 1e3:.3f} ms for {len(sbs)} step(s) (host, synchronized)",
           flush=True)

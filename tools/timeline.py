@@ -19,6 +19,11 @@ for f in glob.glob(d + '/**/*kernel_trace.csv', recursive=True):
     for r in csv.DictReader(open(f)):
         q = r.get('Queue_Id') or r.get('Stream_Id') or '?'
         rows.append((int(r['Start_Timestamp']), int(r['End_Timestamp']), q, r['Kernel_Name']))
+for f in glob.glob(d + '/**/*.db', recursive=True):  # rocprofv3's default (rocpd SQLite) output
+    import sqlite3
+    con = sqlite3.connect(f)
+    for s, e, q, st, n in con.execute("select start, end, queue_id, stream_id, name from kernels"):
+        rows.append((int(s), int(e), f"{q}/{st}", n))
 rows.sort()
 bursts, cur, end = [], [], None
 for s, e, q, n in rows:
