@@ -89,9 +89,10 @@ def parse():
                     help="eds: the upload places each ODS in Q0 of its EDS buffer and the extension "
                          "reads it in place; ods: separate contiguous ODS buffer, the row pass copies Q0")
     ap.add_argument("--phase-reps", type=int, default=10)
-    ap.add_argument("--inflight", type=int, default=1,
+    ap.add_argument("--inflight", type=int, default=2,
                     help="batches in flight: steps go round-robin over this many batches, each with its own "
-                         "buffers and stream (independent blocks back to back)")
+                         "buffers and stream (independent blocks back to back, CEL_FLAG_CALLER_STREAM); "
+                         "1 = one batch, each step split in two chunks on the library's internal streams")
     ap.add_argument("--k512-batch", type=int, default=32,
                     help="with --k 128: k=512 squares per step per GPU of the companion line (0 = off)")
     ap.add_argument("--k512-steps", type=int, default=5)
@@ -928,6 +929,7 @@ def main():
             "parallelism": f"batch{world}",
             "input_layout": ("ODS in Q0 of the EDS buffer (placed by the upload)" if a.input == "eds"
                              else "contiguous ODS buffer"),
+            "batches_in_flight": a.inflight,
         },
         "roofline": {
             "bound": "hbm",
@@ -966,7 +968,7 @@ def main():
         del sb
         torch.cuda.empty_cache()
         m5 = _measure_batch(ctx, local, rank, 512, a.k512_batch, a.k512_steps, 2, 2, a.input,
-                            3, barrier, dist, dev)
+                            3, barrier, dist, dev, a.inflight)
         B5, t5 = a.k512_batch, m5["elapsed"]
         v5 = world * B5 * a.k512_steps / t5
         rs5 = 2048 * 512 * 512 * B5 / m5["t_ext"] / 1e9
@@ -991,7 +993,7 @@ def main():
         # over all ranks through RCCL (all_to_all_single) with its exchange timed alone.
         torch.cuda.empty_cache()
         m4 = _measure_batch(ctx, local, rank, 64, 1024 // world, a.rider_steps, 2, 4, a.input, 3, barrier, dist,
-                            dev)
+                            dev, a.inflight)
         result["k64"] = _k64_fields(world, m4["elapsed"], a.rider_steps, m4["t_ext"], m4["t_com"], 1024 // world)
         del m4
         torch.cuda.empty_cache()

@@ -100,6 +100,7 @@ cel_status cel_ctx_create(int device, cel_ctx** out) {
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_rs[i], hipEventDisableTiming);
   }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_start, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_ext, hipEventDisableTiming);
   for (int i = 0; i < cel_ctx::kPipe && e == hipSuccess; i++) {
     e = hipEventCreateWithFlags(&ctx->ev_dl[i], hipEventDisableTiming);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->dl[i], hipStreamNonBlocking);
@@ -129,6 +130,7 @@ void cel_ctx_destroy(cel_ctx* ctx) {
       if (ctx->ev_rs[i]) (void)hipEventDestroy(ctx->ev_rs[i]);
     }
     if (ctx->ev_start) (void)hipEventDestroy(ctx->ev_start);
+    if (ctx->ev_ext) (void)hipEventDestroy(ctx->ev_ext);
     for (int i = 0; i < cel_ctx::kPipe; i++) {
       if (ctx->dl[i]) {
         (void)hipStreamSynchronize(ctx->dl[i]);
@@ -299,17 +301,23 @@ cel_status cel_dev_extend_batch(cel_ctx* ctx, const void* d_ods, uint32_t n, uin
   const uint64_t ods_sq = (uint64_t)k * k * kShare, eds_sq = 4 * ods_sq, roots_sq = (uint64_t)2 * k * kNode;
   hipStream_t us = pick_stream(ctx, stream);
   if (flags & CEL_FLAG_CALLER_STREAM) {
-    // One chunk on the caller's stream: a caller with several batches in flight on its
-    // own streams overlaps one batch's latency-bound tree tops and DAH with the next
-    // one's bulk itself (profiles/r4_inflight_ab.txt). No internal streams are touched,
-    // so the batches do not meet on shared hardware queues.
-    hipError_t e = launch_extend(static_cast<const uint8_t*>(d_ods), static_cast<uint8_t*>(d_eds), k, n,
-                                 ctx->tables, us);
+    // One chunk on the caller's stream, for a caller with several batches in flight on
+    // its own streams; no internal stream is touched, so the batches do not meet on
+    // shared hardware queues. Each such batch starts when the previous one's extension
+    // is done: its (HBM-bound) extension runs beside the previous batch's leaf hashing,
+    // its hashing beside the previous batch's latency-bound tree top and DAH
+    // (profiles/r4_inflight_ab.txt).
+    hipError_t e = ctx->ext_pending ? hipStreamWaitEvent(us, ctx->ev_ext, 0) : hipSuccess;
+    if (e == hipSuccess)
+      e = launch_extend(static_cast<const uint8_t*>(d_ods), static_cast<uint8_t*>(d_eds), k, n, ctx->tables, us);
+    if (e == hipSuccess) e = hipEventRecord(ctx->ev_ext, us);
     if (e == hipSuccess)
       e = launch_commit(static_cast<const uint8_t*>(d_eds), k, n, static_cast<uint8_t*>(d_row_roots),
                         static_cast<uint8_t*>(d_col_roots), static_cast<uint8_t*>(d_dah), d_status, d_work,
                         (flags & CEL_FLAG_ORDER_CHECK) != 0, us);
-    return e == hipSuccess ? CEL_OK : hip_fail(ctx, e, "extend batch");
+    if (e != hipSuccess) return hip_fail(ctx, e, "extend batch");
+    ctx->ext_pending = true;
+    return CEL_OK;
   }
   hipError_t e = hipEventRecord(ctx->ev_start, us);
   for (uint32_t c = 0; c < plan.nchunks && e == hipSuccess; c++) {

@@ -201,6 +201,10 @@ struct cel_ctx {
   hipStream_t stream = nullptr;
   hipStream_t sub[kPipe] = {nullptr, nullptr, nullptr, nullptr};
   hipEvent_t ev_start = nullptr;
+  // CEL_FLAG_CALLER_STREAM batches: the previous one's extension-done event (recorded
+  // once ext_pending); the next such batch starts after it (api.cpp)
+  hipEvent_t ev_ext = nullptr;
+  bool ext_pending = false;
   hipEvent_t ev_done[kChunks] = {};
   hipEvent_t ev_rs[kChunks] = {};
   // EDS downloads of the host pipeline, one per pipeline stream (beside the hashing)

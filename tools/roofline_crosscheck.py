@@ -6,7 +6,8 @@ with HIP events on the SquareBatch's launch stream, over B squares at once. In t
 those launches are the ones on that stream with the full-batch grids (the timed batch steps
 split B into two chunks on two other streams, so their grids are half the size). This script
 finds the stream of the full-batch rows launch, takes the median duration of every
-(kernel, grid) on it, and rebuilds the line's `roofline.frac` and `roofline_nmt.achieved`.
+(kernel, grid) on it (with batches in flight: after the other batches' last launch, i.e.
+the phase timing alone), and rebuilds the line's `roofline.frac` and `roofline_nmt.achieved`.
 
 usage: python tools/roofline_crosscheck.py <trace dir> <bench json> [k] [B]"""
 import collections
@@ -53,6 +54,14 @@ def main():
     later = [int(r["Start_Timestamp"]) for r in rows if int(r["Start_Timestamp"]) > t0
              and ("k_rs" in r["Kernel_Name"] and r["Kernel_Name"] != rs_kernel)]
     t1 = min(later) if later else float("inf")
+    # --inflight > 1: the timed steps run full-batch launches on every batch's stream, two
+    # batches at once; the phase timing (one batch alone) starts after the last of the
+    # other batches' launches
+    others = {(r["Stream_Id"], r["Queue_Id"]) for r in colc} - {stream}
+    ends = [int(r["End_Timestamp"]) for r in rows if (r["Stream_Id"], r["Queue_Id"]) in others
+            and t0 <= int(r["Start_Timestamp"]) < t1]
+    if ends:
+        t0 = max(ends)
     on = [r for r in rows if (r["Stream_Id"], r["Queue_Id"]) == stream and t0 <= int(r["Start_Timestamp"]) < t1]
     d = collections.defaultdict(list)
     for r in on:
@@ -61,7 +70,8 @@ def main():
     P = out.append
     P(f"# roofline cross-check: rocprofv3 --kernel-trace of `python3 bench.py` vs its JSON line")
     P(f"# trace: {tdir}; line: {bjson}; k={k}, B={B}; launch stream {stream[0]} (queue {stream[1]}),")
-    P(f"# the stream of every full-batch RS rows launch (grid {rows_grid}), from the first of them to the next")
+    P(f"# the stream of the phase timing's full-batch RS launches (rows grid {rows_grid}), from the first of them")
+    P(f"# (with batches in flight: from the other batches' last launch) to the next")
     P(f"# shape's first RS launch ({(t1 - t0) / 1e6 if t1 != float('inf') else 0:.1f} ms); medians over the calls")
     P(f"{'kernel':70s} {'grid':>10s} {'calls':>5s} {'median_us':>10s}")
     for (n, g), v in sorted(d.items(), key=lambda x: -statistics.median(x[1])):

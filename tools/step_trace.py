@@ -23,6 +23,7 @@ ap.add_argument("--k", type=int, default=64)
 ap.add_argument("--batch", type=int, default=128)
 ap.add_argument("--steps", type=int, default=4)
 ap.add_argument("--inflight", type=int, default=1)
+ap.add_argument("--chain", type=int, default=0, help="steps per burst, round-robin over the batches (default: one per batch)")
 a = ap.parse_args()
 from celestia_eds.device import SquareBatch  # noqa: E402
 from celestia_eds.testfactory import random_ods  # noqa: E402
@@ -34,10 +35,10 @@ for j in range(max(1, a.inflight)):
     sbs.append(sb)
 for i in range(a.steps):
     t0 = time.perf_counter()
-    for sb in sbs:
-        sb.extend_and_commit(caller_stream=len(sbs) > 1)
+    for j in range(a.chain or len(sbs)):
+        sbs[j % len(sbs)].extend_and_commit(caller_stream=len(sbs) > 1)
     torch.cuda.synchronize()
-    print(f"burst {i}: {(time.perf_counter() - t0) * 1e3:.3f} ms for {len(sbs)} step(s) (host, synchronized)",
+    print(f"burst {i}: {(time.perf_counter() - t0) * 1e3:.3f} ms for {a.chain or len(sbs)} step(s) (host, synchronized)",
           flush=True)
     time.sleep(0.003)
 for sb in sbs:
