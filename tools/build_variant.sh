@@ -6,8 +6,9 @@
 # (tools/gpu_variants.sh times variants on the GPU box; build_variants/ and variants/ are
 # git-ignored.)
 set -e
-cd "$(dirname "$0")/.."
 name=$1; patch=${2:--}; flags=$3
+[ "$patch" != "-" ] && patch=$(realpath "$patch")
+cd "$(dirname "$0")/.."
 bd=build_variants/$name
 rm -rf $bd
 mkdir -p $bd/src variants
@@ -15,7 +16,7 @@ cp -r celestia-app_amd/csrc $bd/src/csrc
 cp -r include $bd/include
 if [ "$patch" != "-" ]; then
   # the patch names a/celestia-app_amd/csrc/<file> (git diff form): strip two components
-  (cd $bd/src && patch -p2 --quiet < "$OLDPWD/$patch")
+  (cd $bd/src && patch -p2 --quiet < "$patch")
 fi
 HIPCC=/opt/rocm/bin/hipcc
 srcs="api.cpp square.cpp proof.cpp inclusion.cpp inclusion_paths.cpp rs_kernels.hip rs_bitslice.hip rs_axis.hip rs_decode_axis.hip rs_decode_gf16.hip rs_gf16x.hip nmt_kernels.hip repair_kernels.hip"
