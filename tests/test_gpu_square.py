@@ -262,6 +262,36 @@ def test_device_batch(ctx, oracle, k, n, inplace):
     assert np.array_equal(d_eds.download((n, w, w, 512)), eds)
 
 
+@pytest.mark.parametrize("k,n", [(128, 3), (256, 2), (16, 5)])
+def test_device_batch_caller_stream(ctx, oracle, k, n):
+    """CEL_FLAG_CALLER_STREAM at GF(2^8) and GF(2^16) widths and below the axis kernel's
+    range (k=16): the whole batch as one chunk on the ctx's stream (NULL caller stream),
+    twice in a row (the second call waits for the first one's extension), bit-exact."""
+    import ctypes
+    from celestia_eds import _lib
+    from hipmem import DeviceBuffer, synchronize
+    odss = np.stack([random_ods(k, 5100 + 7 * i + k) for i in range(n)])
+    w = 2 * k
+    d_eds = DeviceBuffer(n * w * w * 512, fill=0x3C)
+    d_rr, d_cr = DeviceBuffer(n * w * 90), DeviceBuffer(n * w * 90)
+    d_dah, d_st = DeviceBuffer(n * 32), DeviceBuffer(n * 4, fill=0x7F)
+    d_work = DeviceBuffer(ctx.lib.cel_dev_workspace_size(k, n))
+    ctx.check(ctx.lib.cel_dev_place_ods(ctx.handle, odss.ctypes.data_as(ctypes.c_void_p), n, k, d_eds.ptr, None))
+    for _ in range(2):
+        ctx.check(ctx.lib.cel_dev_extend_batch(ctx.handle, None, n, k, d_eds.ptr, d_rr.ptr, d_cr.ptr, d_dah.ptr,
+                                               d_st.ptr, d_work.ptr, None,
+                                               _lib.FLAG_ORDER_CHECK | _lib.FLAG_CALLER_STREAM))
+    synchronize()
+    eds = d_eds.download((n, w, w, 512))
+    rr, cr = d_rr.download((n, w, 90)), d_cr.download((n, w, 90))
+    dah, st = d_dah.download((n, 32)), d_st.download((n,), np.int32)
+    assert (st == 0).all()
+    for i in range(n):
+        e, r, c, d = oracle.extend_and_commit(odss[i])
+        assert np.array_equal(eds[i], e), f"square {i}: EDS differs"
+        assert np.array_equal(rr[i], r) and np.array_equal(cr[i], c) and dah[i].tobytes() == d
+
+
 @pytest.mark.parametrize("k,region", [(32, "quarter3"), (64, "quarter3"), (128, "quarter3"), (64, "all")])
 def test_parity_namespace_in_ods(ctx, oracle, k, region):
     """ODS shares that carry the parity namespace 0xFF*29 themselves. Their subtrees
