@@ -752,8 +752,7 @@ def _measure_batch(ctx, local, rank, k, B, steps, warmup, n_distinct, layout, ph
     sbs = []
     distinct = [random_ods(k, 1_000_003 * rank + i) for i in range(min(n_distinct, B))]
     for j in range(max(1, inflight)):
-        prio = -1 if (j == 0 and inflight > 1 and os.environ.get("CEL_BENCH_PRIO") == "1") else 0
-        sb = SquareBatch(B, k, device=local, ctx=ctx, ods_in_eds=(layout == "eds"), priority=prio)
+        sb = SquareBatch(B, k, device=local, ctx=ctx, ods_in_eds=(layout == "eds"))
         host = np.stack([distinct[(i + j) % len(distinct)] for i in range(B)])
         sb.load_ods(torch.from_numpy(host))
         del host

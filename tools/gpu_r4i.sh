@@ -1,5 +1,5 @@
 #!/bin/bash
-# Batches in flight: stream priority on the first batch (CEL_BENCH_PRIO=1) vs none, k=64 B=128 / 1024, k=128 B=256.
+# (historical: needs the CEL_BENCH_PRIO hook removed from bench.py after this A/B) Batches in flight: stream priority on the first batch (CEL_BENCH_PRIO=1) vs none, k=64 B=128 / 1024, k=128 B=256.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
