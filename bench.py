@@ -38,12 +38,13 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table)
-# SHA-256 ceiling for the NMT phase: the compression's instruction mix (per 16 rounds with
-# the message schedule: 160 v_alignbit + 64 v_add3 at 4 cycles per wave64 instruction,
-# 96 v_bitop3 at 2.5, 64 VOP2 at 2; the first 16 rounds without schedule) priced at the
-# measured per-op rates of profiles/r1_microbench_valu.txt is ~4.5k cycles per compression
-# per wave: 1024 SIMDs x 2.4 GHz x 64 / 4528 = 34.7 G compressions/s.
-SHA_MIX_CEILING = 1024 * 2.4e9 * 64 / 4528
+# SHA-256 op-mix ceiling: the compression's ISA (576 v_alignbit_b32, 241 v_add3_u32, 352
+# v_bitop3_b32, 245 VOP2 per wave) priced at the dependency-free rate of each op measured
+# alone on the same box as the compression itself (tools/microbench/vop3_banks.hip: 32.15T,
+# 32.3T, 57.0T with conflict-free sources, 61.0T lane-ops/s) -> 28.1 G compressions/s;
+# the compression chained in registers runs 29.2-29.5 G/s on that box, within 5 % of it
+# (profiles/r4_sha_ceiling.txt).
+SHA_MIX_CEILING = 1.0 / (576 / 32.15e12 + 241 / 32.3e12 + 352 / 57.0e12 + 245 / 61.0e12)
 # Measured SHA-256 peak: the NMT kernels' compression (cel::sha256_compress) chained in
 # registers on every lane, no memory traffic, 4-32 waves per SIMD: 29.1-29.6 G
 # compressions/s on two boxes (tools/microbench/sha_rate.hip, profiles/r2_sha_rate.txt).
@@ -51,8 +52,8 @@ SHA_MEASURED_PEAK = 29.4e9
 # The MI355X_MICROARCH.md issue model: every wave64 VALU instruction issues over 2 cycles on
 # a SIMD-32; the compression is 1414 VALU per wave (ISA of the unrolled compression,
 # tools/roofline_crosscheck.py) -> 1024 SIMDs x 2.4 GHz x 64 / (2 x 1414) = 55.6 G/s. The
-# measured per-op rates put v_alignbit / v_add3 (57 % of the mix) at 4 cycles, hence
-# peak_model and the measured peak below it.
+# measured per-op rates put v_alignbit / v_add3 (58 % of the mix) at ~4.8 nominal cycles,
+# hence peak_model and the measured peak below it.
 SHA_GUIDE_CEILING = 1024 * 2.4e9 * 64 / (2 * 1414)
 # Measured HBM traffic of the RS extension (rocprofv3 FETCH_SIZE/WRITE_SIZE passes).
 # (input layout -> profile): ODS in Q0 of the EDS (in place) / separate ODS buffer.
@@ -951,7 +952,7 @@ def main():
             "frac": nmt_rate / SHA_MEASURED_PEAK,
             "peak_model": SHA_MIX_CEILING / 1e9,
             "frac_model": nmt_rate / SHA_MIX_CEILING,
-            "peak_model_basis": "SHA-256 instruction mix at measured per-op VALU rates (profiles/r1_microbench_valu.txt)",
+            "peak_model_basis": "SHA-256 ISA mix at the same box's per-op VALU rates (profiles/r4_sha_ceiling.txt)",
             "peak_guide": SHA_GUIDE_CEILING / 1e9,
             "frac_guide": nmt_rate / SHA_GUIDE_CEILING,
             "peak_guide_basis": "1414 VALU per compression x 2 cycles per wave64 instruction (MI355X_MICROARCH.md "

@@ -22,6 +22,9 @@ SHA_MEASURED_PEAK = 29.4e9
 # compression (tools/microbench/sha_rate.hip k_sha_u, tools/isa_mix.py): alignbit, bitop3,
 # add3, VOP2 (add / lshr / xor / mov)
 SHA_ISA = {"v_alignbit_b32": 576, "v_bitop3_b32": 352, "v_add3_u32": 241, "vop2": 134 + 96 + 15}
+# each op alone, dependency-free, 4 waves per SIMD, on the box of the sha_rate run
+# (tools/microbench/vop3_banks.hip, profiles/r4_sha_ceiling.txt), lane-ops/s
+SHA_OP_RATE = {"v_alignbit_b32": 32.15e12, "v_bitop3_b32": 57.0e12, "v_add3_u32": 32.3e12, "vop2": 61.0e12}
 
 
 def main():
@@ -102,15 +105,14 @@ def main():
     # SHA-256 ceilings for the NMT phase, three ways
     n_valu = sum(SHA_ISA.values())
     guide = 1024 * 2.4e9 * 64 / (2 * n_valu)
-    cyc = 4 * (SHA_ISA["v_alignbit_b32"] + SHA_ISA["v_add3_u32"]) + 2.5 * SHA_ISA["v_bitop3_b32"] + 2 * SHA_ISA["vop2"]
-    model = 1024 * 2.4e9 * 64 / cyc
+    model = 1.0 / sum(SHA_ISA[k] / SHA_OP_RATE[k] for k in SHA_ISA)
     rate = comp / nmt * 1e6
     P("")
     P(f"SHA-256 ceilings ({n_valu} VALU per compression per wave: " + ", ".join(f"{k} {v}" for k, v in SHA_ISA.items()) + ")")
     P(f"  MI355X_MICROARCH.md issue model (every wave64 VALU instruction over 2 cycles, 1024 SIMDs, 2.4 GHz): "
       f"{guide / 1e9:.1f} G/s -> NMT phase frac {rate / guide:.3f}")
-    P(f"  per-op rates measured here (alignbit / add3 4 cycles, bitop3 2.5, VOP2 2; profiles/r1_microbench_valu.txt): "
-      f"{model / 1e9:.1f} G/s -> frac {rate / model:.3f}")
+    P(f"  the mix at each op's dependency-free rate on the compression's box (lane-ops/s: alignbit 32.15T, add3 "
+      f"32.3T, bitop3 57.0T, VOP2 61.0T; profiles/r4_sha_ceiling.txt): {model / 1e9:.1f} G/s -> frac {rate / model:.3f}")
     P(f"  the same compression chained in registers, no memory traffic (profiles/r2_sha_rate.txt): "
       f"{SHA_MEASURED_PEAK / 1e9:.1f} G/s -> frac {rate / SHA_MEASURED_PEAK:.3f}")
     print("\n".join(out))
