@@ -232,10 +232,15 @@ def NewDataAvailabilityHeader(eds):
     return dah
 
 
-def MinShares():
-    """One tail-padding share (go-square shares.TailPaddingShares(1))."""
+def EmptySquareShares():
+    """shares.TailPaddingShares(appconsts.MinShareCount = 1) (data_availability_header.go:197-201)."""
     share = TAIL_PADDING_NAMESPACE + b"\x01" + b"\x00" * 4
     return [share + b"\x00" * (SHARE_SIZE - len(share))]
+
+
+def MinShares():
+    """One tail-padding share: shares.ToBytes(EmptySquareShares()) (data_availability_header.go:192-195)."""
+    return EmptySquareShares()
 
 
 def MinDataAvailabilityHeader():

@@ -82,3 +82,19 @@ def test_share_inputs_checked_before_the_device(fn):
     with pytest.raises(CelError) as ei:
         f(np.zeros((4, 2, 256), np.uint8))
     assert ei.value.status == _lib.EINVAL
+
+
+def test_min_shares_are_one_tail_padding_share():
+    """MinShares = shares.ToBytes(EmptySquareShares()) = one tail-padding share
+    (pkg/da/data_availability_header.go:192-201; go-square TailPaddingShares: the
+    tail-padding namespace, version 0xFF and ID 0xFF*27 || 0xFE, the sequence-start info
+    byte 0x01, a zero sequence length, zeros), as the reference's MinDataAvailabilityHeader
+    extends it (its DAH known answer is checked on the device in test_gpu_square.py). No
+    device."""
+    from celestia_eds import da
+    ms, es = da.MinShares(), da.EmptySquareShares()
+    assert ms == es and len(ms) == 1 and len(ms[0]) == 512
+    s = ms[0]
+    assert s[:29] == b"\xff" * 28 + b"\xfe"
+    assert s[29] == 0x01 and s[30:] == bytes(482)
+    assert da.SquareSize(len(ms)) == 1
