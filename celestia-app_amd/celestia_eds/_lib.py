@@ -30,7 +30,7 @@ EXPORTS = [
     "cel_codec_max_chunks", "cel_codec_name", "cel_codec_validate_chunk_size", "cel_axis_root",
     "cel_nmt_root", "cel_dah_hash", "cel_merkle_hash_slices", "cel_repair", "cel_dev_repair", "cel_debug_schedule_fuzz", "cel_debug_repair_plan", "cel_dev_shard_workspace_size", "cel_dev_shard_rows",
     "cel_dev_shard_cols", "cel_dev_shard_finish", "cel_square_construct", "cel_square_last_error", "cel_square_tx_range",
-    "cel_axis_trees", "cel_dah_tree", "cel_nmt_prove_range", "cel_merkle_aunts", "cel_commitment_paths",
+    "cel_axis_trees", "cel_axis_tree", "cel_dah_tree", "cel_nmt_prove_range", "cel_merkle_aunts", "cel_commitment_paths",
     "cel_get_commitment", "cel_subtree_root_coordinates",
 ]
 
@@ -92,6 +92,7 @@ def load():
             "cel_square_last_error": (ctypes.c_char_p, []),
             "cel_square_tx_range": (i32, [P, P, u32, u32, u32, u32, P, P]),
             "cel_axis_trees": (i32, [P, P, u32, u32, u32, u32, u32, P]),
+            "cel_axis_tree": (i32, [P, P, u32, u32, u32, P]),
             "cel_dah_tree": (i32, [P, P, P, u32, P]),
             "cel_nmt_prove_range": (i32, [P, u32, u32, u32, P, P]),
             "cel_merkle_aunts": (i32, [P, u32, u32, P, P]),

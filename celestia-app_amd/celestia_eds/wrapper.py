@@ -64,6 +64,22 @@ class ErasuredNamespacedMerkleTree:
         return out.tobytes()
 
 
+    def ProveRange(self, start, end):
+        """nmt Proof for the leaf range [start, end) (nmt_wrapper.go:127-130), on a full axis
+        (2k pushed 512-byte shares): every node of the axis tree from the device
+        (cel_axis_tree), the proof nodes picked by cel_nmt_prove_range. start >= end or
+        end > 2k raise, as nmt's validateRange does (ErrInvalidRange)."""
+        from .proof import NMTProof, nmt_prove_range
+        W = 2 * self.squareSize
+        if len(self.leaves) != W or any(len(l) != _lib.NAMESPACE_SIZE + _lib.SHARE_SIZE for l in self.leaves):
+            raise CelError(_lib.EINVAL, f"ProveRange needs the full axis: {W} pushed shares of {_lib.SHARE_SIZE} bytes")
+        cells = np.frombuffer(b"".join(l[_lib.NAMESPACE_SIZE:] for l in self.leaves), np.uint8).copy()
+        tree = np.zeros((2 * W - 1, _lib.NMT_NODE_SIZE), np.uint8)
+        self.ctx.check(self.ctx.lib.cel_axis_tree(self.ctx.handle, _p(cells), self.squareSize, self.axisIndex,
+                                                  _lib.SHARE_SIZE, _p(tree)))
+        return NMTProof(int(start), int(end), nmt_prove_range(tree, int(start), int(end)))
+
+
 def NewErasuredNamespacedMerkleTree(square_size, axis_index):
     return ErasuredNamespacedMerkleTree(square_size, axis_index)
 

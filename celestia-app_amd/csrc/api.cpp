@@ -759,35 +759,20 @@ cel_status cel_merkle_hash_slices(cel_ctx* ctx, const uint8_t* data, const uint6
 // each row's NMT on the CPU to call ProveRange; here the device hashes the trees and
 // hands every node back, and the host proof builders (proof.cpp) only pick nodes.
 
-cel_status cel_axis_trees(cel_ctx* ctx, const uint8_t* eds, uint32_t k, uint32_t share_size, uint32_t axis,
-                          uint32_t first, uint32_t count, uint8_t* nodes_out) {
-  if (!ctx) return CEL_EINVAL;
-  std::lock_guard<std::mutex> lock(ctx->mu);
-  if (!eds || !nodes_out || !count) return fail(ctx, CEL_EINVAL, "nil argument");
-  cel_status st = validate_square(ctx, k, share_size);
-  if (st) return st;
-  const uint32_t W = 2 * k;
-  if (axis > 1 || first >= W || count > W - first) return fail(ctx, CEL_EINVAL, "axis range outside the square");
+// Every node of the NMTs of `idx.size()` axes whose cells sit densely in `cells` (axis a
+// = cells [a * 2k, (a + 1) * 2k)), per axis level-major into nodes_out. ctx->mu held.
+static cel_status dense_axes_trees(cel_ctx* ctx, const std::vector<uint8_t>& cells, const std::vector<int32_t>& idx,
+                                   uint32_t k, uint8_t* nodes_out) {
+  const uint32_t W = 2 * k, count = (uint32_t)idx.size();
   DeviceGuard g(ctx->device);
   hipError_t e = hipSuccess;
-  const size_t cells_b = (size_t)count * W * kShare;
   const size_t nodes = axes_trees_nodes(k, count);
-  uint8_t* d_c = static_cast<uint8_t*>(scratch(ctx, S_IN, cells_b, &e));
+  uint8_t* d_c = static_cast<uint8_t*>(scratch(ctx, S_IN, cells.size(), &e));
   uint32_t* d_n = static_cast<uint32_t*>(scratch(ctx, S_WORK, nodes * kNodeWords * 4, &e));
   int32_t* d_idx = static_cast<int32_t*>(scratch(ctx, S_AUX, (size_t)count * 4, &e));
   if (!d_c || !d_n || !d_idx) return fail(ctx, CEL_ENOMEM, "device allocation failed");
-  // gather the axes densely on the host: rows are contiguous, columns strided
-  std::vector<uint8_t> cells(cells_b);
-  std::vector<int32_t> idx(count);
-  for (uint32_t a = 0; a < count; a++) {
-    idx[a] = (int32_t)(first + a);
-    for (uint32_t j = 0; j < W; j++) {
-      const size_t cell = axis == 0 ? (size_t)(first + a) * W + j : (size_t)j * W + first + a;
-      std::memcpy(&cells[((size_t)a * W + j) * kShare], eds + cell * kShare, kShare);
-    }
-  }
   hipStream_t s = ctx->stream;
-  if ((e = hipMemcpyAsync(d_c, cells.data(), cells_b, hipMemcpyHostToDevice, s)) != hipSuccess ||
+  if ((e = hipMemcpyAsync(d_c, cells.data(), cells.size(), hipMemcpyHostToDevice, s)) != hipSuccess ||
       (e = hipMemcpyAsync(d_idx, idx.data(), (size_t)count * 4, hipMemcpyHostToDevice, s)) != hipSuccess)
     return hip_fail(ctx, e, "H2D");
   if ((e = launch_axes_trees(d_c, k, d_idx, count, d_n, s)) != hipSuccess) return hip_fail(ctx, e, "axis trees");
@@ -808,6 +793,42 @@ cel_status cel_axis_trees(cel_ctx* ctx, const uint8_t* eds, uint32_t k, uint32_t
     if (n == 1) break;
   }
   return CEL_OK;
+}
+
+cel_status cel_axis_trees(cel_ctx* ctx, const uint8_t* eds, uint32_t k, uint32_t share_size, uint32_t axis,
+                          uint32_t first, uint32_t count, uint8_t* nodes_out) {
+  if (!ctx) return CEL_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (!eds || !nodes_out || !count) return fail(ctx, CEL_EINVAL, "nil argument");
+  cel_status st = validate_square(ctx, k, share_size);
+  if (st) return st;
+  const uint32_t W = 2 * k;
+  if (axis > 1 || first >= W || count > W - first) return fail(ctx, CEL_EINVAL, "axis range outside the square");
+  // gather the axes densely on the host: rows are contiguous, columns strided
+  std::vector<uint8_t> cells((size_t)count * W * kShare);
+  std::vector<int32_t> idx(count);
+  for (uint32_t a = 0; a < count; a++) {
+    idx[a] = (int32_t)(first + a);
+    for (uint32_t j = 0; j < W; j++) {
+      const size_t cell = axis == 0 ? (size_t)(first + a) * W + j : (size_t)j * W + first + a;
+      std::memcpy(&cells[((size_t)a * W + j) * kShare], eds + cell * kShare, kShare);
+    }
+  }
+  return dense_axes_trees(ctx, cells, idx, k, nodes_out);
+}
+
+cel_status cel_axis_tree(cel_ctx* ctx, const uint8_t* cells, uint32_t k, uint32_t axis_index, uint32_t share_size,
+                         uint8_t* nodes_out) {
+  if (!ctx) return CEL_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (!cells || !nodes_out) return fail(ctx, CEL_EINVAL, "nil argument");
+  cel_status st = validate_square(ctx, k, share_size);
+  if (st) return st;
+  if (axis_index + 1 > 2 * k)  // nmt_wrapper.go:94-96
+    return fail(ctx, CEL_EPUSHPAST, "pushed past predetermined square size: boundary at " + std::to_string(2 * k) +
+                                        " index at " + std::to_string(axis_index) + " 0");
+  std::vector<uint8_t> dense(cells, cells + (size_t)2 * k * kShare);
+  return dense_axes_trees(ctx, dense, std::vector<int32_t>{(int32_t)axis_index}, k, nodes_out);
 }
 
 cel_status cel_dah_tree(cel_ctx* ctx, const uint8_t* row_roots, const uint8_t* col_roots, uint32_t w,

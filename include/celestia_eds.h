@@ -270,6 +270,12 @@ cel_status cel_debug_repair_plan(const uint8_t* present, uint32_t k, int32_t* so
  * up to the root (leaf j at [j], level-1 node j at [2k + j], ..., root last). */
 cel_status cel_axis_trees(cel_ctx* ctx, const uint8_t* eds, uint32_t k, uint32_t share_size,
                           uint32_t axis, uint32_t first, uint32_t count, uint8_t* nodes_out);
+/* cel_axis_tree: all 4k - 1 nodes of the NMT of one axis from its 2k cells (contiguous
+ * shares, the wrapper's pushed data), axis_index deciding the Q0 namespace rule as in
+ * nmt_wrapper.go:100-107; same layout as one axis of cel_axis_trees. For
+ * ErasuredNamespacedMerkleTree.ProveRange (nmt_wrapper.go:127-130) on a full axis. */
+cel_status cel_axis_tree(cel_ctx* ctx, const uint8_t* cells, uint32_t k, uint32_t axis_index,
+                         uint32_t share_size, uint8_t* nodes_out);
 /* RFC-6962 tree over rowRoots || colRoots (w each, 2w a power of two), every level:
  * nodes_out (4w - 1) * 32 B, level 0 = the 2w leaf hashes, ..., the root last (equal to
  * cel_dah_hash). */

@@ -78,3 +78,38 @@ def test_partial_tree_root(ctx, oracle):
         t.Push(d)
     rc, exp = oracle.nmt_root([d[:29] + d for d in data])
     assert rc == 0 and t.Root() == exp
+
+
+@pytest.mark.parametrize("k", [8, 64])
+def test_prove_range_verifies(ctx, oracle, k):
+    """ErasuredNamespacedMerkleTree.ProveRange (nmt_wrapper.go:127-130) on full axes: the
+    device's axis tree (cel_axis_tree) and the picked proof nodes verify every parity-
+    namespaced range against the tree's root with the nmt verifier pinned by the
+    reference's proof vectors (tests/test_proof.py); a tampered share or node fails;
+    empty / reversed / out-of-range ranges and partial trees raise."""
+    from celestia_eds import CelError
+    from celestia_eds.wrapper import PARITY_NAMESPACE, NewErasuredNamespacedMerkleTree
+    cells = erasured(oracle, k, 300 + k)
+    for axis, ranges in ((0, [(k, 2 * k), (k + 2, k + 5), (2 * k - 1, 2 * k)]),
+                         (k + 1, [(0, 3), (5, 2 * k), (0, 2 * k), (k - 1, k + 1)])):
+        tree = NewErasuredNamespacedMerkleTree(k, axis)
+        for c in cells:
+            tree.Push(c)
+        root = tree.Root()
+        for s, e in ranges:
+            p = tree.ProveRange(s, e)
+            assert (p.Start, p.End) == (s, e)
+            assert p.VerifyInclusion(PARITY_NAMESPACE, cells[s:e], root), (axis, s, e)
+            bad = list(cells[s:e])
+            bad[0] = bytes([bad[0][0] ^ 1]) + bad[0][1:]
+            assert not p.VerifyInclusion(PARITY_NAMESPACE, bad, root)
+            if p.Nodes:
+                p.Nodes[0] = bytes(len(p.Nodes[0]))
+                assert not p.VerifyInclusion(PARITY_NAMESPACE, cells[s:e], root)
+        for s, e in ((3, 3), (4, 2), (0, 2 * k + 1)):
+            with pytest.raises(CelError):
+                tree.ProveRange(s, e)
+    partial = NewErasuredNamespacedMerkleTree(k, 0)
+    partial.Push(cells[0])
+    with pytest.raises(CelError):
+        partial.ProveRange(0, 1)
