@@ -133,6 +133,12 @@ class ExtendedDataSquare:
     def Flattened(self):
         return [self.cells[r, c].tobytes() for r in range(self.Width()) for c in range(self.Width())]
 
+    def FlattenedODS(self):
+        """The original data square (Q0) row-major, as rsmt2d's FlattenedODS; pkg/proof
+        sizes the square from it (pkg/proof/proof.go:84)."""
+        k = self.Width() // 2
+        return [self.cells[r, c].tobytes() for r in range(k) for c in range(k)]
+
     def RowRoots(self):
         if self._row_roots is None:
             self._compute_roots()

@@ -98,3 +98,19 @@ def test_min_shares_are_one_tail_padding_share():
     assert s[:29] == b"\xff" * 28 + b"\xfe"
     assert s[29] == 0x01 and s[30:] == bytes(482)
     assert da.SquareSize(len(ms)) == 1
+
+
+def test_flattened_ods_is_q0_row_major():
+    """ExtendedDataSquare.FlattenedODS (rsmt2d, used by pkg/proof/proof.go:84 to size the
+    square): the k x k original quadrant, row-major; Flattened is the whole 2k x 2k square.
+    Host bookkeeping only, no device."""
+    from celestia_eds.rsmt2d import ExtendedDataSquare
+    k = 4
+    cells = np.zeros((2 * k, 2 * k, 512), np.uint8)
+    for r in range(2 * k):
+        for c in range(2 * k):
+            cells[r, c, :2] = (r, c)
+    eds = ExtendedDataSquare(cells)
+    ods = eds.FlattenedODS()
+    assert len(ods) == k * k and len(eds.Flattened()) == 4 * k * k
+    assert [o[:2] for o in ods] == [bytes((r, c)) for r in range(k) for c in range(k)]
