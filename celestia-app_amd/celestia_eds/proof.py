@@ -545,6 +545,30 @@ TX_NAMESPACE = bytes(28) + b"\x01"
 PFB_NAMESPACE = bytes(28) + b"\x04"
 
 
+def ParseNamespace(raw_shares, start_share, end_share):
+    """pkg/proof/querier.go:134-166: check the end-exclusive share range and that every
+    share in it carries the first one's namespace (29 bytes); return that namespace.
+    Raises CelError(EINVAL) with the reference's messages."""
+    if start_share < 0:
+        raise CelError(_lib.EINVAL, f"start share {start_share} should be positive")
+    if end_share < 0:
+        raise CelError(_lib.EINVAL, f"end share {end_share} should be positive")
+    if end_share <= start_share:
+        raise CelError(_lib.EINVAL,
+                       f"end share {end_share} cannot be lower or equal to the starting share {start_share}")
+    if end_share > len(raw_shares):
+        raise CelError(_lib.EINVAL, f"end share {end_share} is higher than block shares {len(raw_shares)}")
+    first = bytes(raw_shares[start_share][:NS])
+    if len(first) < NS:
+        raise CelError(_lib.ESHORT, "share is too short to contain a namespace")
+    for i, sh in enumerate(raw_shares[start_share:end_share]):
+        ns = bytes(sh[:NS])
+        if ns != first:
+            raise CelError(_lib.EINVAL, f"shares range contain different namespaces at index {i}: "
+                                        f"{first.hex()} and {ns.hex()} ")
+    return first
+
+
 def NewTxInclusionProof(txs, tx_index, max_square_size=128, subtree_root_threshold=64):
     """pkg/proof/proof.go:21-48: square.Construct, FindTxShareRange, then the share proof
     of that range in the tx's namespace (PayForBlob for blob txs, proof.go:50-56)."""

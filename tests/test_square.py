@@ -207,3 +207,29 @@ def test_malformed_txs_match_oracle():
         blk = sorted(txs[i:i + 25], key=lambda t: square_layout.unmarshal_blob_tx(t) is not None)
         k, ref = _oracle_square(blk)
         assert np.array_equal(square.Construct(blk), ref)
+
+
+def test_parse_namespace_block408():
+    """proof.ParseNamespace (pkg/proof/querier.go:134-166) over block 408's square, with the
+    reference's cases (proof_test.go TestNewShareInclusionProof): negative start or end,
+    end <= start, end past the square and a range across two namespaces are errors; tx,
+    PayForBlob and blob ranges return their namespace. Host logic only."""
+    from celestia_eds import CelError, square
+    from celestia_eds.proof import PFB_NAMESPACE, TX_NAMESPACE, ParseNamespace
+    ods = square.Construct(block408_txs())
+    ns = [bytes(s[:29]) for s in ods]
+    n_tx = next(i for i, x in enumerate(ns) if x != TX_NAMESPACE)
+    n_pfb_end = next(i for i in range(n_tx, len(ns)) if ns[i] != PFB_NAMESPACE)
+    assert ns[n_tx] == PFB_NAMESPACE and n_tx > 1
+    for s, e, msg in ((-1, 99, "should be positive"), (0, -99, "should be positive"),
+                      (1, 0, "cannot be lower or equal"), (1, 1, "cannot be lower or equal"),
+                      (0, len(ods) + 1, "higher than block shares"),
+                      (n_tx - 1, n_tx + 1, "different namespaces at index 1")):
+        with pytest.raises(CelError, match=msg):
+            ParseNamespace(ods, s, e)
+    assert ParseNamespace(ods, 0, 1) == TX_NAMESPACE
+    assert ParseNamespace(ods, 0, n_tx) == TX_NAMESPACE
+    assert ParseNamespace(ods, n_tx, n_pfb_end) == PFB_NAMESPACE
+    blob = ns[n_pfb_end]
+    blob_end = next(i for i in range(n_pfb_end, len(ns)) if ns[i] != blob)
+    assert ParseNamespace(ods, n_pfb_end, blob_end) == blob
