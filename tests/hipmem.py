@@ -61,6 +61,14 @@ class DeviceBuffer:
         _ck(hip().hipMemcpy(out.ctypes.data_as(ctypes.c_void_p), self.ptr, out.nbytes, _D2H), "D2H")
         return out
 
+    def download_at(self, offset, shape, dtype=np.uint8):
+        """D2H of shape's bytes starting `offset` bytes into the buffer."""
+        out = np.empty(shape, dtype)
+        assert offset + out.nbytes <= self.nbytes
+        src = ctypes.c_void_p(self.ptr.value + offset)
+        _ck(hip().hipMemcpy(out.ctypes.data_as(ctypes.c_void_p), src, out.nbytes, _D2H), "D2H")
+        return out
+
     def free(self):
         if self.ptr:
             hip().hipFree(self.ptr)

@@ -431,3 +431,52 @@ def test_batches_in_flight_on_two_streams(ctx, oracle, k, n):
     a.check()
     b.check()
     synchronize()
+
+
+def test_bench_shape_batches_in_flight(ctx, oracle):
+    """The bench's full shape (BASELINE config 2): 256 k=128 squares per batch, two
+    batches in flight on two caller streams (CEL_FLAG_CALLER_STREAM, bench --inflight 2),
+    steps alternating. Size-independent properties against the oracle: every square's
+    DAH and its 512 roots equal those of its source (4 distinct ODSs, as the bench
+    replicates them), a sampled square's whole EDS is bit-exact, and every status is 0."""
+    import ctypes
+    from celestia_eds import _lib
+    from hipmem import DeviceBuffer, Stream, synchronize
+    k, n, w = 128, 256, 256
+    distinct = [random_ods(k, 9100 + i) for i in range(4)]
+    expect = [oracle.extend_and_commit(d) for d in distinct]
+    host = np.stack([distinct[i % 4] for i in range(n)])
+
+    class Batch:
+        def __init__(self, shift):
+            self.s = Stream()
+            self.eds = DeviceBuffer(n * w * w * 512)
+            self.rr, self.cr = DeviceBuffer(n * w * 90), DeviceBuffer(n * w * 90)
+            self.dah, self.st = DeviceBuffer(n * 32), DeviceBuffer(n * 4, fill=0x7F)
+            self.work = DeviceBuffer(ctx.lib.cel_dev_workspace_size(k, n))
+            self.src = host if shift == 0 else np.ascontiguousarray(np.roll(host, shift, axis=0))
+            self.shift = shift
+            ctx.check(ctx.lib.cel_dev_place_ods(ctx.handle, self.src.ctypes.data_as(ctypes.c_void_p), n, k,
+                                                self.eds.ptr, self.s.ptr))
+
+        def step(self):
+            ctx.check(ctx.lib.cel_dev_extend_batch(ctx.handle, None, n, k, self.eds.ptr, self.rr.ptr, self.cr.ptr,
+                                                   self.dah.ptr, self.st.ptr, self.work.ptr, self.s.ptr,
+                                                   _lib.FLAG_ORDER_CHECK | _lib.FLAG_CALLER_STREAM))
+
+    a, b = Batch(0), Batch(1)
+    for _ in range(2):
+        a.step()
+        b.step()
+    synchronize()
+    for bt in (a, b):
+        dah, st = bt.dah.download((n, 32)), bt.st.download((n,), np.int32)
+        rr, cr = bt.rr.download((n, w, 90)), bt.cr.download((n, w, 90))
+        assert (st == 0).all()
+        for i in range(n):
+            e = expect[(i - bt.shift) % 4]
+            assert dah[i].tobytes() == e[3], f"square {i}: DAH differs"
+            assert np.array_equal(rr[i], e[1]) and np.array_equal(cr[i], e[2]), f"square {i}: roots differ"
+        for sq in (0, 137, n - 1):
+            eds = bt.eds.download_at(sq * w * w * 512, (w, w, 512))
+            assert np.array_equal(eds, expect[(sq - bt.shift) % 4][0]), f"square {sq}: EDS differs"
