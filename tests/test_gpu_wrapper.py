@@ -113,3 +113,22 @@ def test_prove_range_verifies(ctx, oracle, k):
     partial.Push(cells[0])
     with pytest.raises(CelError):
         partial.ProveRange(0, 1)
+
+
+def test_axis_tree_abi_errors(ctx):
+    """cel_axis_tree validates before any device work: axis index past the square
+    (EPUSHPAST, nmt_wrapper.go:94-96), non-power-of-two width (ENOTPOW2), share size other
+    than 512 (ECHUNK), nil pointers (EINVAL)."""
+    import ctypes
+    from celestia_eds import _lib
+    k = 8
+    cells = np.zeros((2 * k, 512), np.uint8)
+    out = np.zeros((4 * k - 1, 90), np.uint8)
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    f = ctx.lib.cel_axis_tree
+    assert f(ctx.handle, P(cells), k, 2 * k, 512, P(out)) == _lib.EPUSHPAST
+    assert f(ctx.handle, P(cells), 6, 0, 512, P(out)) == _lib.ENOTPOW2
+    assert f(ctx.handle, P(cells), k, 0, 256, P(out)) == _lib.ECHUNK
+    assert f(ctx.handle, None, k, 0, 512, P(out)) == _lib.EINVAL
+    assert f(ctx.handle, P(cells), k, 0, 512, None) == _lib.EINVAL
+    assert f(ctx.handle, P(cells), k, 2 * k - 1, 512, P(out)) == _lib.OK
