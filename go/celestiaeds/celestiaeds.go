@@ -439,6 +439,44 @@ func (c *Context) GetCommitment(eds []byte, k, start, blobShareLen, subtreeRootT
 	return out, nil
 }
 
+// ProveRange is ErasuredNamespacedMerkleTree.ProveRange (pkg/wrapper/nmt_wrapper.go:127-130)
+// for a full axis: cells are the axis's 2k shares (what the wrapper tree was pushed),
+// axisIndex its index; the device hashes every node of the axis tree (cel_axis_tree) and
+// cel_nmt_prove_range picks the proof nodes of [start, end), which
+// nmt.NewInclusionProof(start, end, nodes, true) turns into the nmt.Proof the wrapper
+// returns (IgnoreMaxNamespace, as wrapper.NewErasuredNamespacedMerkleTree sets it).
+func (c *Context) ProveRange(cells [][]byte, k, axisIndex, start, end int) ([][]byte, error) {
+	if len(cells) != 2*k || !deviceShares(cells) {
+		return nil, &StatusError{Status: int(C.CEL_EINVAL), Msg: "ProveRange needs the axis's 2k shares of 512 bytes"}
+	}
+	flat := make([]byte, 0, 2*k*ShareSize)
+	for _, s := range cells {
+		flat = append(flat, s...)
+	}
+	tree := make([]byte, (4*k-1)*NmtNodeSize)
+	if err := c.call(func() C.cel_status {
+		return C.cel_axis_tree(c.ctx, (*C.uint8_t)(unsafe.Pointer(&flat[0])), C.uint32_t(k), C.uint32_t(axisIndex),
+			C.CEL_SHARE_SIZE, (*C.uint8_t)(unsafe.Pointer(&tree[0])))
+	}); err != nil {
+		return nil, err
+	}
+	var n C.uint32_t
+	if st := C.cel_nmt_prove_range((*C.uint8_t)(unsafe.Pointer(&tree[0])), C.uint32_t(2*k), C.uint32_t(start),
+		C.uint32_t(end), nil, &n); st != C.CEL_OK {
+		return nil, &StatusError{Status: int(st), Msg: fmt.Sprintf("invalid range [%d, %d) over %d leaves", start, end, 2*k)}
+	}
+	out := make([]byte, int(n)*NmtNodeSize)
+	if n > 0 {
+		C.cel_nmt_prove_range((*C.uint8_t)(unsafe.Pointer(&tree[0])), C.uint32_t(2*k), C.uint32_t(start),
+			C.uint32_t(end), (*C.uint8_t)(unsafe.Pointer(&out[0])), &n)
+	}
+	nodes := make([][]byte, int(n))
+	for i := range nodes {
+		nodes[i] = out[i*NmtNodeSize : (i+1)*NmtNodeSize]
+	}
+	return nodes, nil
+}
+
 // Repair wraps cel_repair, the device pass behind rsmt2d.ExtendedDataSquare.Repair
 // (rsmt2d v0.14.0 extendeddatacrossword.go): flat is the flattened 2k x 2k square
 // (missing cells may hold anything), present[i] != 0 marks known cells. On success
