@@ -64,20 +64,48 @@ class ErasuredNamespacedMerkleTree:
         return out.tobytes()
 
 
+    def _subtree_root(self, lo, hi):
+        """NMT root over pushed leaves [lo, hi) on the device (cel_nmt_root)."""
+        ln = len(self.leaves[lo])
+        if any(len(l) != ln for l in self.leaves[lo:hi]):
+            raise CelError(_lib.EINVAL, "device NMT root needs equal-length leaves")
+        buf = np.frombuffer(b"".join(self.leaves[lo:hi]), np.uint8).copy()
+        out = np.zeros(_lib.NMT_NODE_SIZE, np.uint8)
+        self.ctx.check(self.ctx.lib.cel_nmt_root(self.ctx.handle, _p(buf), hi - lo, ln, _p(out), 0))
+        return out.tobytes()
+
     def ProveRange(self, start, end):
-        """nmt Proof for the leaf range [start, end) (nmt_wrapper.go:127-130), on a full axis
-        (2k pushed 512-byte shares): every node of the axis tree from the device
-        (cel_axis_tree), the proof nodes picked by cel_nmt_prove_range. start >= end or
-        end > 2k raise, as nmt's validateRange does (ErrInvalidRange)."""
-        from .proof import NMTProof, nmt_prove_range
+        """nmt Proof for the leaf range [start, end) over the pushed leaves
+        (nmt_wrapper.go:127-130). A full axis of 512-byte shares with 2k a power of two
+        takes every node of its tree from the device (cel_axis_tree) and the proof nodes
+        picked by cel_nmt_prove_range; any other tree (a partial or odd-width one, as the
+        reference test's square sizes 1..16) collects nmt's proof nodes, the roots of the
+        maximal subtrees outside the range under its split rule (largest power of two
+        below the width), each hashed on the device (cel_nmt_root). start >= end,
+        start < 0 or end past the leaves raise, as nmt's validateRange does."""
+        from .proof import NMTProof, _split_point, nmt_prove_range
+        start, end, n = int(start), int(end), len(self.leaves)
+        if start < 0 or start >= end or end > n:
+            raise CelError(_lib.EINVAL, f"invalid proof range [{start}, {end}) over {n} leaves")
         W = 2 * self.squareSize
-        if len(self.leaves) != W or any(len(l) != _lib.NAMESPACE_SIZE + _lib.SHARE_SIZE for l in self.leaves):
-            raise CelError(_lib.EINVAL, f"ProveRange needs the full axis: {W} pushed shares of {_lib.SHARE_SIZE} bytes")
-        cells = np.frombuffer(b"".join(l[_lib.NAMESPACE_SIZE:] for l in self.leaves), np.uint8).copy()
-        tree = np.zeros((2 * W - 1, _lib.NMT_NODE_SIZE), np.uint8)
-        self.ctx.check(self.ctx.lib.cel_axis_tree(self.ctx.handle, _p(cells), self.squareSize, self.axisIndex,
-                                                  _lib.SHARE_SIZE, _p(tree)))
-        return NMTProof(int(start), int(end), nmt_prove_range(tree, int(start), int(end)))
+        full = (n == W and W & (W - 1) == 0 and
+                all(len(l) == _lib.NAMESPACE_SIZE + _lib.SHARE_SIZE for l in self.leaves))
+        if full:
+            cells = np.frombuffer(b"".join(l[_lib.NAMESPACE_SIZE:] for l in self.leaves), np.uint8).copy()
+            tree = np.zeros((2 * W - 1, _lib.NMT_NODE_SIZE), np.uint8)
+            self.ctx.check(self.ctx.lib.cel_axis_tree(self.ctx.handle, _p(cells), self.squareSize, self.axisIndex,
+                                                      _lib.SHARE_SIZE, _p(tree)))
+            return NMTProof(start, end, nmt_prove_range(tree, start, end))
+
+        def collect(lo, hi):
+            if hi <= start or lo >= end:
+                return [self._subtree_root(lo, hi)]
+            if start <= lo and hi <= end:
+                return []
+            k = _split_point(hi - lo)
+            return collect(lo, lo + k) + collect(lo + k, hi)
+
+        return NMTProof(start, end, collect(0, n))
 
 
 def NewErasuredNamespacedMerkleTree(square_size, axis_index):

@@ -86,7 +86,8 @@ def test_prove_range_verifies(ctx, oracle, k):
     device's axis tree (cel_axis_tree) and the picked proof nodes verify every parity-
     namespaced range against the tree's root with the nmt verifier pinned by the
     reference's proof vectors (tests/test_proof.py); a tampered share or node fails;
-    empty / reversed / out-of-range ranges and partial trees raise."""
+    empty / reversed / out-of-range ranges raise; a partial tree proves over its pushed
+    leaves."""
     from celestia_eds import CelError
     from celestia_eds.wrapper import PARITY_NAMESPACE, NewErasuredNamespacedMerkleTree
     cells = erasured(oracle, k, 300 + k)
@@ -109,10 +110,14 @@ def test_prove_range_verifies(ctx, oracle, k):
         for s, e in ((3, 3), (4, 2), (0, 2 * k + 1)):
             with pytest.raises(CelError):
                 tree.ProveRange(s, e)
+    # a partial tree proves over what was pushed (nmt keeps no width), past it raises
     partial = NewErasuredNamespacedMerkleTree(k, 0)
-    partial.Push(cells[0])
+    for c in cells[:3]:
+        partial.Push(c)
+    p = partial.ProveRange(1, 2)
+    assert p.VerifyInclusion(cells[1][:29], [cells[1]], partial.Root())
     with pytest.raises(CelError):
-        partial.ProveRange(0, 1)
+        partial.ProveRange(0, 4)
 
 
 def test_axis_tree_abi_errors(ctx):
@@ -132,3 +137,24 @@ def test_axis_tree_abi_errors(ctx):
     assert f(ctx.handle, None, k, 0, 512, P(out)) == _lib.EINVAL
     assert f(ctx.handle, P(cells), k, 0, 512, None) == _lib.EINVAL
     assert f(ctx.handle, P(cells), k, 2 * k - 1, 512, P(out)) == _lib.OK
+
+
+def test_prove_range_every_leaf(ctx, oracle):
+    """nmt_wrapper_test.go:152-180 TestErasuredNamespacedMerkleTree_ProveRange: square sizes
+    1..16 (odd widths included), axis 0, the k raw shares and their k parity shares; for
+    every leaf i ProveRange(i, i+1) is a non-empty proof that verifies against the tree's
+    root under the leaf's namespace (its own for i < k, the parity namespace otherwise).
+    Power-of-two widths take the cel_axis_tree path, the rest the subtree-root path; both
+    give nmt's node order."""
+    from celestia_eds.wrapper import PARITY_NAMESPACE, NewErasuredNamespacedMerkleTree
+    for k in range(1, 17):
+        data = erasured(oracle, k, 700 + k)[: 2 * k]
+        tree = NewErasuredNamespacedMerkleTree(k, 0)
+        for d in data:
+            tree.Push(d)
+        root = tree.Root()
+        for i in range(2 * k):
+            p = tree.ProveRange(i, i + 1)
+            assert p.Nodes, (k, i)
+            ns = data[i][:29] if i < k else PARITY_NAMESPACE
+            assert p.VerifyInclusion(ns, [data[i]], root), (k, i)
