@@ -158,3 +158,34 @@ def test_prove_range_every_leaf(ctx, oracle):
             assert p.Nodes, (k, i)
             ns = data[i][:29] if i < k else PARITY_NAMESPACE
             assert p.VerifyInclusion(ns, [data[i]], root), (k, i)
+
+
+def test_out_of_order_nmt_like_the_malicious_tree(ctx, oracle):
+    """test/util/malicious/app_test.go:23-62 TestOutOfOrderNMT through the C ABI: over 64
+    namespaced shares (square size 64, axis 0) the order-checking root (the honest wrapper)
+    and the unchecked root (the malicious tree's hasher, malicious/hasher.go) agree on
+    ordered data; shuffled, the honest path refuses (CEL_EORDER) and the unchecked one
+    returns a 90-byte root that differs from the ordered one and equals the oracle's NMT
+    over the same shuffled leaves."""
+    import ctypes
+    from celestia_eds import _lib
+    rng = np.random.default_rng(62)
+    data = [bytes(d) for d in random_ods(8, 64).reshape(-1, 512)[:64]]
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+
+    def root(shares, flags):
+        leaves = np.frombuffer(b"".join(s[:29] + s for s in shares), np.uint8).copy()  # Q0: ns || share
+        out = np.zeros(90, np.uint8)
+        st = ctx.lib.cel_nmt_root(ctx.handle, P(leaves), len(shares), 29 + 512, P(out), flags)
+        return st, out.tobytes()
+
+    st_good, good = root(data, _lib.FLAG_ORDER_CHECK)
+    st_mal, mal = root(data, 0)
+    assert st_good == st_mal == _lib.OK and good == mal
+    shuffled = [data[i] for i in rng.permutation(64)]
+    st, _ = root(shuffled, _lib.FLAG_ORDER_CHECK)
+    assert st == _lib.EORDER
+    st, bad = root(shuffled, 0)
+    assert st == _lib.OK and len(bad) == 90 and bad != good
+    rc, exp = oracle.nmt_root([s[:29] + s for s in shuffled], check_order=False)
+    assert rc == 0 and bad == exp
