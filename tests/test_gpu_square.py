@@ -480,3 +480,24 @@ def test_bench_shape_batches_in_flight(ctx, oracle):
         for sq in (0, 137, n - 1):
             eds = bt.eds.download_at(sq * w * w * 512, (w, w, 512))
             assert np.array_equal(eds, expect[(sq - bt.shift) % 4][0]), f"square {sq}: EDS differs"
+
+
+@pytest.mark.parametrize("seed,n_normal,n_blob", [(31, 3, 0), (32, 30, 8), (33, 120, 40), (34, 0, 90), (35, 400, 5)])
+def test_prepare_process_consistency(ctx, oracle, seed, n_normal, n_blob):
+    """app/test/fuzz_abci_test.go:26-160 in spirit (PrepareProposal's data root must be what
+    ProcessProposal recomputes, across square sizes): random blocks of normal and blob txs
+    -> the product's square.Construct -> device ExtendShares + DAH, against an independent
+    path: the oracle's square layout (oracle/square_layout.py) -> the oracle's extension
+    and DAH. Both the square and the data root must agree."""
+    import square_layout
+    from celestia_eds import da, square
+    from square_inputs import random_block
+    txs = random_block(seed, n_normal, n_blob)
+    ods = square.Construct(txs)
+    k_o, shares_o = square_layout.build_square(txs)
+    assert np.array_equal(ods, np.frombuffer(b"".join(shares_o), np.uint8).reshape(-1, 512))
+    k = int(round(len(ods) ** 0.5))
+    assert k == k_o
+    dah = da.ComputeDataAvailabilityHeader(list(ods))
+    _, _, _, d = oracle.extend_and_commit(np.ascontiguousarray(ods).reshape(k, k, 512))
+    assert dah.Hash() == d
