@@ -19,7 +19,7 @@ if [ "$patch" != "-" ]; then
   (cd $bd/src && patch -p2 --quiet < "$patch")
 fi
 HIPCC=/opt/rocm/bin/hipcc
-srcs="api.cpp api_repair.cpp square.cpp proof.cpp inclusion.cpp inclusion_paths.cpp rs_kernels.hip rs_bitslice.hip rs_axis.hip rs_decode_axis.hip rs_decode_gf16.hip rs_gf16x.hip nmt_kernels.hip repair_kernels.hip"
+srcs="api.cpp api_repair.cpp api_shard.cpp api_trees.cpp square.cpp proof.cpp inclusion.cpp inclusion_paths.cpp rs_kernels.hip rs_bitslice.hip rs_axis.hip rs_decode_axis.hip rs_decode_gf16.hip rs_gf16x.hip nmt_kernels.hip repair_kernels.hip"
 objs=""
 for f in $srcs; do
   extra=""
