@@ -738,6 +738,18 @@ def measure_rowshard(k, world, rank, local, dist, dev, steps, warmup, barrier, d
     return f
 
 
+def _rider(result, name, fn):
+    """result[name] = fn(), a part of the line beside the headline batch. A part that
+    raises is reported as {"error": ...} instead of losing the whole line (every rank runs
+    the same parts with the same shapes, so a failure is symmetric)."""
+    try:
+        result[name] = fn()
+    except Exception as e:  # noqa: BLE001
+        result[name] = {"error": f"{type(e).__name__}: {e}"[:400]}
+        print(f"bench: {name} failed: {e!r}", file=sys.stderr, flush=True)
+    torch.cuda.empty_cache()
+
+
 def _measure_batch(ctx, local, rank, k, B, steps, warmup, n_distinct, layout, phase_reps, barrier, dist, dev,
                    inflight=1):
     """Time `steps` batch steps of B k x k squares resident in HBM (barrier + synchronize
@@ -967,23 +979,25 @@ def main():
         dah128 = sb.dah.cpu().numpy()
         del sb
         torch.cuda.empty_cache()
-        m5 = _measure_batch(ctx, local, rank, 512, a.k512_batch, a.k512_steps, 2, 2, a.input,
-                            3, barrier, dist, dev, a.inflight)
-        B5, t5 = a.k512_batch, m5["elapsed"]
-        v5 = world * B5 * a.k512_steps / t5
-        rs5 = 2048 * 512 * 512 * B5 / m5["t_ext"] / 1e9
-        comp5 = (60 * 512 * 512 + 4 * 512 - 2) * B5 / m5["t_com"]
-        result["k512"] = {
-            "workload": "k=512 ODS (GF(2^16)) -> EDS + 2048 NMT roots + DAH, batch replay",
-            "value": v5, "unit": "squares/s", "ods_gbps": v5 * 512 * 512 * 512 / 1e9,
-            "squares_per_step_per_gpu": B5, "steps": a.k512_steps,
-            "ms_per_step": t5 / a.k512_steps * 1e3,
-            "rs_frac_hbm": rs5 / HBM_PEAK_GBS, "rs_avg_launch_us": m5["t_ext"] * 1e6,
-            "nmt_frac_sha_peak": comp5 / SHA_MEASURED_PEAK, "nmt_frac_sha_mix": comp5 / SHA_MIX_CEILING,
-            "nmt_avg_launch_us": m5["t_com"] * 1e6,
-        }
-        del m5
-        torch.cuda.empty_cache()
+
+        def k512():
+            m5 = _measure_batch(ctx, local, rank, 512, a.k512_batch, a.k512_steps, 2, 2, a.input,
+                                3, barrier, dist, dev, a.inflight)
+            B5, t5 = a.k512_batch, m5["elapsed"]
+            v5 = world * B5 * a.k512_steps / t5
+            rs5 = 2048 * 512 * 512 * B5 / m5["t_ext"] / 1e9
+            comp5 = (60 * 512 * 512 + 4 * 512 - 2) * B5 / m5["t_com"]
+            return {
+                "workload": "k=512 ODS (GF(2^16)) -> EDS + 2048 NMT roots + DAH, batch replay",
+                "value": v5, "unit": "squares/s", "ods_gbps": v5 * 512 * 512 * 512 / 1e9,
+                "squares_per_step_per_gpu": B5, "steps": a.k512_steps,
+                "ms_per_step": t5 / a.k512_steps * 1e3,
+                "rs_frac_hbm": rs5 / HBM_PEAK_GBS, "rs_avg_launch_us": m5["t_ext"] * 1e6,
+                "nmt_frac_sha_peak": comp5 / SHA_MEASURED_PEAK, "nmt_frac_sha_mix": comp5 / SHA_MIX_CEILING,
+                "nmt_avg_launch_us": m5["t_com"] * 1e6,
+            }
+
+        _rider(result, "k512", k512)
         sb = None
     else:
         dah128 = None
@@ -991,21 +1005,25 @@ def main():
         # Configs 4 and 3 in the same run, so one driver N-GPU command measures configs 2, 3
         # and 4: 1024 k=64 squares split over the ranks, and one k=512 square row-sharded
         # over all ranks through RCCL (all_to_all_single) with its exchange timed alone.
-        torch.cuda.empty_cache()
-        m4 = _measure_batch(ctx, local, rank, 64, 1024 // world, a.rider_steps, 2, 4, a.input, 3, barrier, dist,
-                            dev, a.inflight)
-        result["k64"] = _k64_fields(world, m4["elapsed"], a.rider_steps, m4["t_ext"], m4["t_com"], 1024 // world)
-        del m4
-        torch.cuda.empty_cache()
-        result["rowshard512"] = measure_rowshard(512, world, rank, local, dist, dev, a.rider_steps, 2, barrier,
-                                                 a.depth)
-        torch.cuda.empty_cache()
+        def k64():
+            m4 = _measure_batch(ctx, local, rank, 64, 1024 // world, a.rider_steps, 2, 4, a.input, 3, barrier,
+                                dist, dev, a.inflight)
+            return _k64_fields(world, m4["elapsed"], a.rider_steps, m4["t_ext"], m4["t_com"], 1024 // world)
+
+        _rider(result, "k64", k64)
+        _rider(result, "rowshard512", lambda: measure_rowshard(512, world, rank, local, dist, dev, a.rider_steps, 2,
+                                                               barrier, a.depth))
     if rank == 0 and world == 1 and a.k == 128 and not a.no_host_io:
-        result["host_io"] = measure_host_io(ctx, a.k)
+        _rider(result, "host_io", lambda: measure_host_io(ctx, a.k))
     if rank == 0 and world == 1 and not a.no_cpu:
         dah_dev = dah128 if dah128 is not None else sb.dah.cpu().numpy()
-        result["cpu_baseline"], parity = cpu_baseline_batch(k, distinct, dah_dev, a.cpu_seconds)
-        result["parity_vs_cpu"] = bool(parity)
+
+        def cpu():
+            base, parity = cpu_baseline_batch(k, distinct, dah_dev, a.cpu_seconds)
+            result["parity_vs_cpu"] = bool(parity)
+            return base
+
+        _rider(result, "cpu_baseline", cpu)
     if REHEARSE:
         result["config"]["rehearsal"] = "all ranks on cuda:0, gloo with host staging: not a multi-GPU measurement"
     if rank == 0:
