@@ -23,4 +23,4 @@ cat gpurun_out/${tag}_bench_repair512.json
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --marker-trace --stats -d gpurun_out/${tag}_prof -o b --output-format csv -- \
   python3 bench.py --steps 5 --warmup 2 --no-host-io --k512-batch 8 > gpurun_out/${tag}_bench_prof.json 2>/dev/null || exit $?
-python3 tools/kstats.py gpurun_out/${tag}_prof | head -16
+python3 tools/kstats.py gpurun_out/${tag}_prof > gpurun_out/${tag}_kstats.txt && head -16 gpurun_out/${tag}_kstats.txt
