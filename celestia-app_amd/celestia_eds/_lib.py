@@ -18,6 +18,7 @@ OK, EINVAL, ENOTPOW2, ECHUNK, ETOOBIG, EORDER, ETOOFEW, EBYZANTINE, EUNREPAIRABL
 FLAG_ORDER_CHECK = 0x1
 FLAG_PARITY_ONLY = 0x2
 FLAG_CALLER_STREAM = 0x4
+FLAG_SHARD_EXCHANGE = 0x8
 SHARE_SIZE = 512
 NAMESPACE_SIZE = 29
 NMT_NODE_SIZE = 90
@@ -32,6 +33,9 @@ EXPORTS = [
     "cel_dev_shard_cols", "cel_dev_shard_finish", "cel_square_construct", "cel_square_last_error", "cel_square_tx_range",
     "cel_axis_trees", "cel_axis_tree", "cel_dah_tree", "cel_nmt_prove_range", "cel_merkle_aunts", "cel_commitment_paths",
     "cel_get_commitment", "cel_subtree_root_coordinates",
+    "cel_extend_sharded", "cel_shard_plan_create", "cel_shard_plan_destroy", "cel_shard_plan_transport",
+    "cel_shard_plan_last_error", "cel_shard_plan_upload", "cel_shard_plan_run", "cel_shard_plan_wait",
+    "cel_extend_batch_multi", "cel_probe_sha256", "cel_probe_hbm_copy",
 ]
 
 _lib = None
@@ -99,6 +103,17 @@ def load():
             "cel_commitment_paths": (i32, [u32, u32, u32, u32, P, P, P, u32, P]),
             "cel_get_commitment": (i32, [P, P, u32, u32, u32, u32, u32, P]),
             "cel_subtree_root_coordinates": (i32, [u32, u32, u32, u32, P, P, u32, P]),
+            "cel_extend_sharded": (i32, [P, u32, P, u32, u32, P, P, P, P, u32]),
+            "cel_shard_plan_create": (i32, [P, u32, u32, u32, PP]),
+            "cel_shard_plan_destroy": (None, [P]),
+            "cel_shard_plan_transport": (ctypes.c_char_p, [P]),
+            "cel_shard_plan_last_error": (ctypes.c_char_p, [P]),
+            "cel_shard_plan_upload": (i32, [P, P]),
+            "cel_shard_plan_run": (i32, [P]),
+            "cel_shard_plan_wait": (i32, [P, P, P, P, P]),
+            "cel_extend_batch_multi": (i32, [P, u32, P, u32, u32, u32, P, P, P, P, P, u32]),
+            "cel_probe_sha256": (i32, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
+            "cel_probe_hbm_copy": (i32, [P, u64, ctypes.POINTER(ctypes.c_double)]),
         }
         for name, (res, args) in sigs.items():
             fn = getattr(l, name)

@@ -1,0 +1,104 @@
+// C ABI of the same-run probes (include/celestia_eds.h, cel_probe_*): the ceilings a report
+// prices the hot path against, measured on the ctx's device in the same process as the
+// measurement itself, so a line from another box or clock carries its own denominators.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "api_common.hpp"
+#include "cel_internal.hpp"
+
+using namespace cel;
+using namespace cel::abi;
+
+namespace {
+
+// Best of `reps` timed launches of fn on s (one untimed warm-up launch first), in seconds.
+template <class F>
+hipError_t best_time(F fn, int reps, hipStream_t s, double* secs) {
+  hipEvent_t a = nullptr, b = nullptr;
+  hipError_t e = hipEventCreate(&a);
+  if (e == hipSuccess) e = hipEventCreate(&b);
+  if (e == hipSuccess) e = fn();
+  double best = 1e30;
+  for (int i = 0; i < reps && e == hipSuccess; i++) {
+    if ((e = hipEventRecord(a, s)) != hipSuccess || (e = fn()) != hipSuccess || (e = hipEventRecord(b, s)) != hipSuccess ||
+        (e = hipEventSynchronize(b)) != hipSuccess)
+      break;
+    float ms = 0;
+    if ((e = hipEventElapsedTime(&ms, a, b)) != hipSuccess) break;
+    best = std::min(best, (double)ms * 1e-3);
+  }
+  if (a) (void)hipEventDestroy(a);
+  if (b) (void)hipEventDestroy(b);
+  *secs = best;
+  return e;
+}
+
+}  // namespace
+
+extern "C" {
+
+cel_status cel_probe_sha256(cel_ctx* ctx, double* g_compressions_per_s, double* shader_mhz) {
+  if (!ctx || !g_compressions_per_s) return CEL_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  DeviceGuard g(ctx->device);
+  int cus = 0, wall_khz = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess ||
+      hipDeviceGetAttribute(&wall_khz, hipDeviceAttributeWallClockRate, ctx->device) != hipSuccess)
+    return fail(ctx, CEL_EDEVICE, "device attributes");
+  const uint32_t blocks = (uint32_t)cus * 16;  // 16 workgroups of 256 per CU (sha_rate.hip sweep)
+  const int n = 64;                            // compressions per lane
+  const uint32_t waves = blocks * 4;
+  hipError_t e = hipSuccess;
+  uint8_t* buf = static_cast<uint8_t*>(scratch(ctx, S_AUX, (size_t)blocks * 256 * 4 + (size_t)waves * 16, &e));
+  if (!buf) return fail(ctx, CEL_ENOMEM, "device allocation failed");
+  uint32_t* out = reinterpret_cast<uint32_t*>(buf);
+  auto* clk = reinterpret_cast<unsigned long long*>(buf + (size_t)blocks * 256 * 4);
+  hipStream_t s = ctx->stream;
+  double secs = 0;
+  e = best_time([&] { return launch_probe_sha(out, clk, blocks, n, s); }, 5, s, &secs);
+  if (e != hipSuccess) return hip_fail(ctx, e, "sha probe");
+  *g_compressions_per_s = (double)blocks * 256 * n / secs / 1e9;
+  if (shader_mhz) {
+    // the last launch's waves: shader-clock ticks per constant-rate tick
+    std::vector<unsigned long long> h((size_t)waves * 2);
+    if ((e = hipMemcpy(h.data(), clk, h.size() * 8, hipMemcpyDeviceToHost)) != hipSuccess)
+      return hip_fail(ctx, e, "sha probe clock");
+    double ticks = 0, real = 0;
+    for (uint32_t i = 0; i < waves; i++) {
+      ticks += (double)h[2 * i];
+      real += (double)h[2 * i + 1];
+    }
+    *shader_mhz = real > 0 ? ticks / real * (wall_khz / 1e3) : 0.0;
+  }
+  return CEL_OK;
+}
+
+cel_status cel_probe_hbm_copy(cel_ctx* ctx, uint64_t bytes, double* gbps) {
+  if (!ctx || !gbps || bytes < 2 * 16) return CEL_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  DeviceGuard g(ctx->device);
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess)
+    return fail(ctx, CEL_EDEVICE, "device attributes");
+  const uint64_t half = (bytes / 2) & ~(uint64_t)4095;  // read half, write half
+  void *src = nullptr, *dst = nullptr;
+  hipError_t e = hipMalloc(&src, half);
+  if (e == hipSuccess) e = hipMalloc(&dst, half);
+  if (e == hipSuccess) e = hipMemsetAsync(src, 0x5A, half, ctx->stream);
+  double secs = 0;
+  if (e == hipSuccess)
+    e = best_time([&] { return launch_probe_copy(src, dst, half, (uint32_t)cus * 8, ctx->stream); }, 5, ctx->stream,
+                  &secs);
+  if (src) (void)hipFree(src);
+  if (dst) (void)hipFree(dst);
+  if (e != hipSuccess) return e == hipErrorOutOfMemory ? fail(ctx, CEL_ENOMEM, "device allocation failed")
+                                                       : hip_fail(ctx, e, "hbm probe");
+  *gbps = 2.0 * (double)half / secs / 1e9;
+  return CEL_OK;
+}
+
+}  // extern "C"

@@ -15,6 +15,69 @@
 #include "api_common.hpp"
 #include "cel_internal.hpp"
 
+namespace cel {
+
+// Step 1 of a rank (shared by cel_dev_shard_rows and the in-library plan, api_multi.cpp):
+// row-encode the rank's k/nranks ODS rows into the all-to-all send layout.
+hipError_t shard_rows_enqueue(const DeviceTables& t, const uint8_t* ods_rows, uint32_t k, uint32_t nranks,
+                              uint8_t* send, hipStream_t s) {
+  const uint32_t rows = k / nranks, w = 2 * k / nranks;
+  const uint64_t blk = (uint64_t)rows * w * kShare;  // one destination rank's block
+  uint32_t wlog = 0;
+  while ((1u << wlog) < w) wlog++;
+  RsGeom gm{};
+  gm.in = ods_rows;
+  gm.in_sq = (uint64_t)rows * k * kShare;
+  gm.in_axis = (uint64_t)k * kShare;
+  gm.in_shard = kShare;
+  // Q0 cell (i, j) -> block j / w, row i, slot j % w; Q1 cell (i, k + j) likewise
+  gm.dcopy = send;
+  gm.dc_sq = gm.in_sq;
+  gm.dc_axis = (uint64_t)w * kShare;
+  gm.dc_shard = kShare;
+  gm.dc_blk = blk;
+  gm.out = send + (uint64_t)(k / w) * blk + (uint64_t)(k % w) * kShare;
+  gm.out_sq = gm.in_sq;
+  gm.out_axis = (uint64_t)w * kShare;
+  gm.out_shard = kShare;
+  gm.out_blk = blk;
+  gm.blk_log = wlog;
+  gm.n = k;
+  gm.len = kShare;
+  gm.axes = rows;
+  gm.nsq = 1;
+  return launch_rs_encode(gm, t, s);
+}
+
+// Step 2 of a rank: column-encode its slab in place, hash the slab's leaves once, build its
+// column-root and row-subtree records.
+hipError_t shard_cols_enqueue(const DeviceTables& t, uint8_t* slab, uint32_t k, uint32_t nranks, uint32_t rank,
+                              uint32_t* col_rec, uint32_t* row_sub, int32_t* status, void* work, bool order_check,
+                              hipStream_t s) {
+  const uint32_t w = 2 * k / nranks;
+  RsGeom gm{};
+  gm.in = slab;
+  gm.in_sq = (uint64_t)2 * k * w * kShare;
+  gm.in_axis = kShare;
+  gm.in_shard = (uint64_t)w * kShare;
+  gm.out = slab + (uint64_t)k * w * kShare;
+  gm.out_sq = gm.in_sq;
+  gm.out_axis = kShare;
+  gm.out_shard = (uint64_t)w * kShare;
+  gm.n = k;
+  gm.len = kShare;
+  gm.axes = w;
+  gm.nsq = 1;
+  // Column pass, then the slab's leaves and trees. Hashing the top half's leaves on a
+  // second stream beside the column pass measured no faster (profiles/r3_rank_latency.txt).
+  hipError_t e = launch_rs_encode(gm, t, s);
+  if (e == hipSuccess) e = launch_slab_leaves(slab, k, rank * w, w, 0, 2 * k, work, order_check, true, s);
+  if (e == hipSuccess) e = launch_slab_trees(k, w, col_rec, row_sub, status, work, s);
+  return e;
+}
+
+}  // namespace cel
+
 using namespace cel;
 using namespace cel::abi;
 
@@ -43,33 +106,8 @@ cel_status cel_dev_shard_rows(cel_ctx* ctx, const void* d_ods_rows, uint32_t k, 
   cel_status st = validate_shard(ctx, k, nranks);
   if (st) return st;
   DeviceGuard g(ctx->device);
-  const uint32_t rows = k / nranks, w = 2 * k / nranks;
-  const uint64_t blk = (uint64_t)rows * w * kShare;  // one destination rank's block
-  uint8_t* send = static_cast<uint8_t*>(d_send);
-  uint32_t wlog = 0;
-  while ((1u << wlog) < w) wlog++;
-  RsGeom gm{};
-  gm.in = static_cast<const uint8_t*>(d_ods_rows);
-  gm.in_sq = (uint64_t)rows * k * kShare;
-  gm.in_axis = (uint64_t)k * kShare;
-  gm.in_shard = kShare;
-  // Q0 cell (i, j) -> block j / w, row i, slot j % w; Q1 cell (i, k + j) likewise
-  gm.dcopy = send;
-  gm.dc_sq = gm.in_sq;
-  gm.dc_axis = (uint64_t)w * kShare;
-  gm.dc_shard = kShare;
-  gm.dc_blk = blk;
-  gm.out = send + (uint64_t)(k / w) * blk + (uint64_t)(k % w) * kShare;
-  gm.out_sq = gm.in_sq;
-  gm.out_axis = (uint64_t)w * kShare;
-  gm.out_shard = kShare;
-  gm.out_blk = blk;
-  gm.blk_log = wlog;
-  gm.n = k;
-  gm.len = kShare;
-  gm.axes = rows;
-  gm.nsq = 1;
-  hipError_t e = launch_rs_encode(gm, ctx->tables, pick_stream(ctx, stream));
+  hipError_t e = shard_rows_enqueue(ctx->tables, static_cast<const uint8_t*>(d_ods_rows), k, nranks,
+                                    static_cast<uint8_t*>(d_send), pick_stream(ctx, stream));
   return e == hipSuccess ? CEL_OK : hip_fail(ctx, e, "shard rows");
 }
 
@@ -82,32 +120,10 @@ cel_status cel_dev_shard_cols(cel_ctx* ctx, void* d_slab, uint32_t k, uint32_t n
   if (st) return st;
   if (rank >= nranks) return fail(ctx, CEL_EINVAL, "rank out of range");
   DeviceGuard g(ctx->device);
-  const uint32_t w = 2 * k / nranks;
-  uint8_t* slab = static_cast<uint8_t*>(d_slab);
-  hipStream_t s = pick_stream(ctx, stream);
-  RsGeom gm{};
-  gm.in = slab;
-  gm.in_sq = (uint64_t)2 * k * w * kShare;
-  gm.in_axis = kShare;
-  gm.in_shard = (uint64_t)w * kShare;
-  gm.out = slab + (uint64_t)k * w * kShare;
-  gm.out_sq = gm.in_sq;
-  gm.out_axis = kShare;
-  gm.out_shard = (uint64_t)w * kShare;
-  gm.n = k;
-  gm.len = kShare;
-  gm.axes = w;
-  gm.nsq = 1;
-  // Column pass, then the slab's leaves and trees. Hashing the top half's leaves on a
-  // second stream beside the column pass measured no faster (profiles/r3_rank_latency.txt).
-  const bool order = (flags & CEL_FLAG_ORDER_CHECK) != 0;
-  hipError_t e;
-  if ((e = launch_rs_encode(gm, ctx->tables, s)) != hipSuccess) return hip_fail(ctx, e, "shard cols");
-  if ((e = launch_slab_leaves(slab, k, rank * w, w, 0, 2 * k, d_work, order, true, s)) != hipSuccess ||
-      (e = launch_slab_trees(k, w, static_cast<uint32_t*>(d_col_rec), static_cast<uint32_t*>(d_row_sub), d_status,
-                             d_work, s)) != hipSuccess)
-    return hip_fail(ctx, e, "shard commit");
-  return CEL_OK;
+  hipError_t e = shard_cols_enqueue(ctx->tables, static_cast<uint8_t*>(d_slab), k, nranks, rank,
+                                    static_cast<uint32_t*>(d_col_rec), static_cast<uint32_t*>(d_row_sub), d_status,
+                                    d_work, (flags & CEL_FLAG_ORDER_CHECK) != 0, pick_stream(ctx, stream));
+  return e == hipSuccess ? CEL_OK : hip_fail(ctx, e, "shard cols");
 }
 
 cel_status cel_dev_shard_finish(cel_ctx* ctx, const void* d_gathered, uint32_t k, uint32_t nranks, void* d_row_roots,

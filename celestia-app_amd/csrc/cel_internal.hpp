@@ -134,11 +134,23 @@ hipError_t launch_slab_leaves(const uint8_t* slab, uint32_t k, uint32_t c0, uint
                               void* work, bool order_check, bool init_bad, hipStream_t s);
 hipError_t launch_slab_trees(uint32_t k, uint32_t w, uint32_t* col_rec, uint32_t* row_sub, int32_t* status,
                              void* work, hipStream_t s);
+// A rank's two device steps (api_shard.cpp): the row pass into the all-to-all send layout
+// [nranks][k/nranks][w][512], and the column pass + slab commit over [2k][w][512].
+hipError_t shard_rows_enqueue(const DeviceTables& t, const uint8_t* ods_rows, uint32_t k, uint32_t nranks,
+                              uint8_t* send, hipStream_t s);
+hipError_t shard_cols_enqueue(const DeviceTables& t, uint8_t* slab, uint32_t k, uint32_t nranks, uint32_t rank,
+                              uint32_t* col_rec, uint32_t* row_sub, int32_t* status, void* work, bool order_check,
+                              hipStream_t s);
 size_t shard_finish_workspace_size(uint32_t k, uint32_t nranks);
 // gathered: [nranks][2k + w + 1] records, rank order (row subtrees, column roots, status).
 hipError_t launch_shard_finish(const uint32_t* gathered, uint32_t k, uint32_t nranks, uint8_t* row_roots,
                                uint8_t* col_roots, uint8_t* dah, int32_t* status, void* work, bool order_check,
                                hipStream_t s);
+
+// Same-run probes (probe_kernels.hip): SHA-256 chained in registers (out: blocks*256 words,
+// clk: 2 counters per wave), and a streaming copy of `bytes` (a multiple of 16).
+hipError_t launch_probe_sha(uint32_t* out, unsigned long long* clk, uint32_t blocks, int n, hipStream_t s);
+hipError_t launch_probe_copy(const void* src, void* dst, uint64_t bytes, uint32_t blocks, hipStream_t s);
 
 // Repair helpers (repair_kernels.hip, nmt_kernels.hip).
 hipError_t launch_gather_axes(const uint8_t* eds, const uint8_t* mask, uint32_t W, const int32_t* idx, int is_col,
@@ -223,4 +235,7 @@ struct cel_ctx {
   // before each enqueue point, an idle kernel of 0..fuzz_max_us microseconds.
   uint64_t fuzz_state = 0;
   uint32_t fuzz_max_us = 0;
+  // cel_extend_sharded's plan (buffers, streams, RCCL communicators), kept while the device
+  // list, k and flags stay the same (api_multi.cpp)
+  cel_shard_plan* shard_cache = nullptr;
 };

@@ -63,7 +63,13 @@ typedef int32_t cel_status;
                                        imported square at the input shares): 3/4 of the PCIe bytes */
 #define CEL_FLAG_CALLER_STREAM 0x4u /* cel_dev_extend_batch: the whole batch as one chunk on the
                                        caller's stream, no internal streams (a caller keeping
-                                       several batches in flight on its own streams) */
+                                       several batches in flight on its own streams). Such
+                                       batches on one ctx are chained: each starts its extension
+                                       after the previous CALLER_STREAM batch's extension on that
+                                       ctx has finished (an event wait, whatever stream either
+                                       ran on), so its extension runs beside the previous batch's
+                                       hashing. Independent pipelines that must not be ordered
+                                       use one ctx each. */
 
 #define CEL_SHARE_SIZE 512u
 #define CEL_NAMESPACE_SIZE 29u
@@ -169,6 +175,68 @@ cel_status cel_dev_shard_cols(cel_ctx* ctx, void* d_slab, uint32_t k, uint32_t n
 cel_status cel_dev_shard_finish(cel_ctx* ctx, const void* d_gathered, uint32_t k, uint32_t nranks, void* d_row_roots,
                                 void* d_col_roots, void* d_dah, int32_t* d_status, void* d_work, void* stream,
                                 uint32_t flags);
+
+/* --------------------------------------- multi-GPU inside the library (configs 3, 4)
+ * One process, one host thread, several devices: ctxs[0..ngpu) as cel_ctx_create made them.
+ * The collectives run inside the library over RCCL: one communicator rank per device
+ * (ncclCommInitAll), every rank's sends / receives / all-gathers issued inside
+ * ncclGroupStart / ncclGroupEnd. librccl.so.1 is loaded (dlopen) by the first plan over
+ * distinct devices; the single-device entry points never need it. RCCL refuses two ranks on
+ * one device, so a plan whose ctxs repeat a device moves the same blocks with device copies
+ * instead (transport "copy": the same schedule, e.g. N ranks rehearsed on one GPU).
+ *
+ * cel_extend_sharded: da.ExtendShares + da.NewDataAvailabilityHeader
+ * (data_availability_header.go:65-75, :44-63) for ONE square row-sharded over ngpu devices
+ * (config 3): rank r row-encodes ODS rows [r k/N, (r+1) k/N) straight into
+ * the all-to-all layout, grouped ncclSend / ncclRecv transpose the column blocks (k/N x 2k/N
+ * cells per peer), each rank column-encodes and commits its [2k][2k/N] slab, one ncclAllGather
+ * of 96-byte record blocks, rank 0 combines the row subtrees and hashes the DAH. Same
+ * arguments and outputs as cel_extend_shares (ods: k*k*512 host bytes; eds_out nullable, with
+ * CEL_FLAG_PARITY_ONLY its Q0 cells are not written). k = 256 or 512 (Leopard GF(2^16)), ngpu a
+ * power of two <= k. The plan (buffers, streams, communicators) is kept in ctxs[0] for the
+ * next call with the same device list, k and flags; ctxs[0]'s lock serialises such calls. */
+cel_status cel_extend_sharded(cel_ctx* const* ctxs, uint32_t ngpu, const uint8_t* ods, uint32_t k,
+                              uint32_t share_size, uint8_t* eds_out, uint8_t* row_roots, uint8_t* col_roots,
+                              uint8_t* dah, uint32_t flags);
+/* The same square as an explicit plan, for callers that keep ODSs resident or several squares
+ * in flight (each plan has its own streams and communicators):
+ *   create   per-rank buffers, streams, tables and the communicators (the expensive part);
+ *   upload   ods (k*k*512 bytes, host or device memory) -> each rank's row block;
+ *   run      one square, asynchronous on the ranks' streams;
+ *   wait     sync, then (each nullable) the EDS (from every rank's column slab), the roots and
+ *            the DAH (rank 0); returns the square's status (CEL_EORDER) or a device error.
+ * flags: CEL_FLAG_ORDER_CHECK, CEL_FLAG_PARITY_ONLY (wait's eds_out), CEL_FLAG_SHARD_EXCHANGE. */
+typedef struct cel_shard_plan cel_shard_plan;
+#define CEL_FLAG_SHARD_EXCHANGE 0x8u /* ngpu = 1: a separate send buffer and the all-to-all run through
+                                        the communicator (self send / receive) instead of the row pass
+                                        writing the slab in place (tests the N > 1 exchange on one GPU) */
+cel_status cel_shard_plan_create(cel_ctx* const* ctxs, uint32_t ngpu, uint32_t k, uint32_t flags,
+                                 cel_shard_plan** out);
+void cel_shard_plan_destroy(cel_shard_plan* plan);
+const char* cel_shard_plan_transport(const cel_shard_plan* plan); /* "rccl" or "copy" */
+const char* cel_shard_plan_last_error(const cel_shard_plan* plan);
+cel_status cel_shard_plan_upload(cel_shard_plan* plan, const uint8_t* ods);
+cel_status cel_shard_plan_run(cel_shard_plan* plan);
+cel_status cel_shard_plan_wait(cel_shard_plan* plan, uint8_t* eds_out, uint8_t* row_roots, uint8_t* col_roots,
+                               uint8_t* dah);
+/* Config 4 over several devices: cel_extend_batch's arguments, the n squares split into ngpu
+ * contiguous ranges (sizes differ by at most one) each extended by cel_extend_batch on ctxs[i]
+ * from its own host thread, so every device's PCIe copies and kernels run side by side
+ * (page-locked buffers from cel_host_alloc keep the copies asynchronous). ctxs may repeat a
+ * device. Returns the first failing range's status (its message in ctxs[0]). */
+cel_status cel_extend_batch_multi(cel_ctx* const* ctxs, uint32_t ngpu, const uint8_t* ods, uint32_t n, uint32_t k,
+                                  uint32_t share_size, uint8_t* eds_out, uint8_t* row_roots, uint8_t* col_roots,
+                                  uint8_t* dah, int32_t* status_out, uint32_t flags);
+
+/* ------------------------------------------------------- same-run probes
+ * The ceilings a report prices the hot path against, measured on ctx's device in the same
+ * process (bench.py's line): cel_probe_sha256 runs the NMT kernels' SHA-256 compression
+ * chained in registers on every lane with no memory traffic (G compressions/s, best of 5
+ * launches) and reports the sustained shader clock over that launch (MHz, nullable: shader
+ * clock ticks per constant-rate tick of every wave); cel_probe_hbm_copy streams a copy over
+ * `bytes` of HBM (half read, half written) and reports read + write GB/s (best of 5). */
+cel_status cel_probe_sha256(cel_ctx* ctx, double* g_compressions_per_s, double* shader_mhz);
+cel_status cel_probe_hbm_copy(cel_ctx* ctx, uint64_t bytes, double* gbps);
 
 /* ------------------------------------------------------ rsmt2d.Codec surface
  * Leopard RS (klauspost/reedsolomon v1.12.1 New(n, n, WithLeopardGF(true))):
