@@ -641,12 +641,17 @@ def _rank_device(local):
     return 0 if REHEARSE else local
 
 
+IDLE_GROUP = None  # gloo group: ranks wait here (no GPU work) while rank 0 drives every GPU
+
+
 def _init_dist(dev):
+    global IDLE_GROUP
     import torch.distributed as dist
     if REHEARSE:
         dist.init_process_group("gloo")
     else:
         dist.init_process_group("nccl", device_id=dev)
+    IDLE_GROUP = dist.new_group(backend="gloo")
     return dist
 
 
@@ -736,6 +741,133 @@ def measure_rowshard(k, world, rank, local, dist, dev, steps, warmup, barrier, d
     if piped:
         f["pipelined"] = piped
     return f
+
+
+def measure_probe(ctx):
+    """Same-run ceilings on this rank's device (cel_probe_sha256 / cel_probe_hbm_copy): the
+    SHA-256 compression in registers (G/s) with the sustained shader clock over that launch,
+    and a streaming copy's read + write GB/s. The line's fractions use them beside the
+    fixed constants, so a box with another clock or HBM shows it in its own denominators."""
+    from celestia_eds.multi import probe
+    return probe(ctx, 4 << 30)
+
+
+def _lib_devices(world):
+    """The devices rank 0 drives in one process for the library riders: one per rank (all on
+    cuda:0 in a --rehearse run, where the plan's transport is device copies)."""
+    return [_rank_device(r) for r in range(world)]
+
+
+def _lib_ctxs(devs):
+    from celestia_eds import Context, default_context
+    return [default_context(d) for d in devs]
+
+
+def measure_rowshard_lib(k, world, steps, warmup, depth):
+    """Config 3 through the library (cel_shard_plan_*): this one process drives the square
+    over all N devices, the all-to-all and record all-gather issued by the library over RCCL
+    (ncclCommInitAll communicators, grouped ncclSend / ncclRecv, ncclAllGather). One square in
+    flight (run + wait: the latency of cel_extend_sharded minus the PCIe upload), then `depth`
+    plans in flight (own streams and communicators each). The ODS rows are resident (uploaded
+    once before the clock); wait() brings back the roots, the DAH and the status."""
+    from celestia_eds.multi import ShardPlan
+    from celestia_eds.testfactory import random_ods
+    devs = _lib_devices(world)
+    ctxs = _lib_ctxs(devs)
+    plans = [ShardPlan(ctxs, k) for _ in range(max(1, depth))]
+    for i, p in enumerate(plans):
+        p.upload(random_ods(k, 512 + i))
+    p0 = plans[0]
+
+    def one():
+        p0.run()
+        p0.wait()
+
+    def piped():
+        for p in plans:
+            p.run()
+        for p in plans:
+            p.wait()
+
+    def clock(fn, n):
+        for _ in range(warmup):
+            fn()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            fn()
+        return time.perf_counter() - t0
+
+    t1 = clock(one, steps)
+    tp = clock(piped, steps)
+    transport = p0.transport
+    for p in plans:
+        p.close()
+    return {"workload": f"config 3: one k={k} square row-sharded over {len(devs)} GPU(s) by ONE process through "
+                        "the C ABI (cel_shard_plan_*: in-library RCCL all-to-all + all-gather)",
+            "driver": "library", "transport": transport, "devices": devs,
+            "value": steps / t1, "unit": "squares/s", "latency_ms": t1 / steps * 1e3, "steps": steps,
+            "scaling": "strong",
+            "pipelined": {"squares_in_flight": len(plans), "value": len(plans) * steps / tp, "unit": "squares/s",
+                          "ms_per_square": tp / (len(plans) * steps) * 1e3}}
+
+
+def measure_k64_lib(world, steps, warmup, inflight):
+    """Config 4 through the library from ONE process: 1024 k=64 squares resident in HBM, 1024/N
+    per device, every device's batches enqueued by this thread (cel_dev_extend_batch on one
+    ctx per device, CEL_FLAG_CALLER_STREAM, `inflight` batches per device); the clock brackets
+    every device's synchronize."""
+    from celestia_eds.device import SquareBatch
+    from celestia_eds.testfactory import random_ods
+    devs = _lib_devices(world)
+    ctxs = _lib_ctxs(devs)
+    B = 1024 // len(devs)
+    distinct = [random_ods(64, 7000 + i) for i in range(4)]
+    host = torch.from_numpy(np.stack([distinct[i % 4] for i in range(B)]))
+    sbs = []
+    for d, c in zip(devs, ctxs):
+        mine = []
+        for _ in range(max(1, inflight)):
+            sb = SquareBatch(B, 64, device=d, ctx=c, ods_in_eds=True)
+            sb.load_ods(host)
+            mine.append(sb)
+        sbs.append(mine)
+    del host
+
+    def sync():
+        for d in sorted(set(devs)):
+            torch.cuda.synchronize(d)
+
+    piped = inflight > 1
+    for i in range(warmup):
+        for mine in sbs:
+            mine[i % len(mine)].extend_and_commit(caller_stream=piped)
+    sync()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        for mine in sbs:
+            mine[i % len(mine)].extend_and_commit(caller_stream=piped)
+    sync()
+    el = time.perf_counter() - t0
+    for mine in sbs:
+        for sb in mine:
+            assert (sb.status.cpu().numpy() == 0).all()
+    del sbs
+    return {"workload": f"config 4: 1024 independent k=64 squares, {B} per GPU on {len(devs)} GPU(s), all "
+                        "enqueued by ONE process through the C ABI (cel_dev_extend_batch per device ctx)",
+            "driver": "library", "devices": devs, "value": 1024 * steps / el, "unit": "squares/s",
+            "ms_per_step": el / steps * 1e3, "steps": steps, "squares_per_step_per_gpu": B, "scaling": "strong"}
+
+
+def _library_riders(result, a, world, rank, dist):
+    """Rank 0 alone drives every GPU of the job through the library (one process, as a Go
+    node would): configs 3 and 4. The other ranks wait on a gloo barrier, which puts no work
+    on their GPUs, so rank 0's kernels and RCCL have the devices to themselves."""
+    if rank == 0:
+        _rider(result, "rowshard512_lib", lambda: measure_rowshard_lib(512, world, a.rider_steps, 2, a.depth))
+        if world > 1:
+            _rider(result, "k64_lib", lambda: measure_k64_lib(world, a.rider_steps, 2, a.inflight))
+    if dist is not None:
+        dist.barrier(group=IDLE_GROUP)
 
 
 def _rider(result, name, fn):
@@ -905,6 +1037,11 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    probe = None
+    try:
+        probe = measure_probe(ctx)
+    except Exception as e:  # noqa: BLE001  (the line keeps its fixed-constant fractions)
+        print(f"bench: probe failed: {e!r}", file=sys.stderr, flush=True)
     m = _measure_batch(ctx, local, rank, a.k, a.batch, a.steps, a.warmup, a.distinct, a.input,
                        a.phase_reps, barrier, dist, dev, a.inflight)
     k, B, elapsed, t_ext, t_com = a.k, a.batch, m["elapsed"], m["t_ext"], m["t_com"]
@@ -972,6 +1109,16 @@ def main():
             "avg_launch_us": t_com * 1e6,
         },
     }
+    if probe:
+        # same-run denominators (cel_probe_*, before the timed region, this rank's device)
+        result["probe"] = {**probe, "basis": "cel_probe_sha256 (NMT compression chained in registers, 16 WG/CU; "
+                                             "shader clock = s_memtime ticks per s_memrealtime tick over that "
+                                             "launch) and cel_probe_hbm_copy (4 GiB streaming copy, read + write)"}
+        result["roofline"]["achievable"] = probe["hbm_copy_gbps"]
+        result["roofline"]["frac_of_achievable_hbm"] = rs_gbs / probe["hbm_copy_gbps"]
+        result["roofline_nmt"]["peak_same_run"] = probe["sha256_gcomp_per_s"]
+        result["roofline_nmt"]["frac_same_run"] = nmt_rate / 1e9 / probe["sha256_gcomp_per_s"]
+        result["shader_mhz"] = probe["shader_mhz"]
 
     if a.k == 128 and a.k512_batch > 0:
         # The metric names k=128 and k=512: a short GF(2^16) batch rides along with the
@@ -994,6 +1141,7 @@ def main():
                 "ms_per_step": t5 / a.k512_steps * 1e3,
                 "rs_frac_hbm": rs5 / HBM_PEAK_GBS, "rs_avg_launch_us": m5["t_ext"] * 1e6,
                 "nmt_frac_sha_peak": comp5 / SHA_MEASURED_PEAK, "nmt_frac_sha_mix": comp5 / SHA_MIX_CEILING,
+                "nmt_frac_same_run": comp5 / 1e9 / probe["sha256_gcomp_per_s"] if probe else None,
                 "nmt_avg_launch_us": m5["t_com"] * 1e6,
             }
 
@@ -1011,8 +1159,10 @@ def main():
             return _k64_fields(world, m4["elapsed"], a.rider_steps, m4["t_ext"], m4["t_com"], 1024 // world)
 
         _rider(result, "k64", k64)
-        _rider(result, "rowshard512", lambda: measure_rowshard(512, world, rank, local, dist, dev, a.rider_steps, 2,
-                                                               barrier, a.depth))
+        if world > 1:  # per-rank processes, torch.distributed's RCCL (at N = 1: rowshard512_lib alone)
+            _rider(result, "rowshard512", lambda: measure_rowshard(512, world, rank, local, dist, dev, a.rider_steps,
+                                                                   2, barrier, a.depth))
+        _library_riders(result, a, world, rank, dist)
     if rank == 0 and world == 1 and a.k == 128 and not a.no_host_io:
         _rider(result, "host_io", lambda: measure_host_io(ctx, a.k))
     if rank == 0 and world == 1 and not a.no_cpu:

@@ -561,8 +561,14 @@ def ParseNamespace(raw_shares, start_share, end_share):
     first = bytes(raw_shares[start_share][:NS])
     if len(first) < NS:
         raise CelError(_lib.ESHORT, "share is too short to contain a namespace")
+    # Each share's length is checked where the reference parses its namespace (querier.go:
+    # 157-160, share.Namespace() per share). The mismatch message prints the namespaces in
+    # hex; the reference formats them with %v (a byte-slice dump), so only the text before
+    # the colon matches it.
     for i, sh in enumerate(raw_shares[start_share:end_share]):
         ns = bytes(sh[:NS])
+        if len(ns) < NS:
+            raise CelError(_lib.ESHORT, "share is too short to contain a namespace")
         if ns != first:
             raise CelError(_lib.EINVAL, f"shares range contain different namespaces at index {i}: "
                                         f"{first.hex()} and {ns.hex()} ")

@@ -89,10 +89,15 @@ cel_status cel_probe_hbm_copy(cel_ctx* ctx, uint64_t bytes, double* gbps) {
   hipError_t e = hipMalloc(&src, half);
   if (e == hipSuccess) e = hipMalloc(&dst, half);
   if (e == hipSuccess) e = hipMemsetAsync(src, 0x5A, half, ctx->stream);
-  double secs = 0;
-  if (e == hipSuccess)
-    e = best_time([&] { return launch_probe_copy(src, dst, half, (uint32_t)cus * 8, ctx->stream); }, 5, ctx->stream,
-                  &secs);
+  // the fastest of {non-temporal, default policy} x {8, 16 workgroups per CU}
+  double secs = 1e30;
+  for (int v = 0; v < 4 && e == hipSuccess; v++) {
+    double t = 0;
+    const bool nt = v & 1;
+    const uint32_t blocks = (uint32_t)cus * (v < 2 ? 8 : 16);
+    e = best_time([&] { return launch_probe_copy(src, dst, half, blocks, nt, ctx->stream); }, 5, ctx->stream, &t);
+    secs = std::min(secs, t);
+  }
   if (src) (void)hipFree(src);
   if (dst) (void)hipFree(dst);
   if (e != hipSuccess) return e == hipErrorOutOfMemory ? fail(ctx, CEL_ENOMEM, "device allocation failed")

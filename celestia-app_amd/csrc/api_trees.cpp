@@ -28,7 +28,7 @@ cel_status cel_axis_root(cel_ctx* ctx, const uint8_t* cells, uint32_t k, uint32_
   std::lock_guard<std::mutex> lock(ctx->mu);
   if (!cells || !root_out || !k) return fail(ctx, CEL_EINVAL, "nil argument");
   if (share_size != kShare) return fail(ctx, CEL_ECHUNK, "share size must be 512 on the device path");
-  if (axis_index + 1 > 2 * k)  // nmt_wrapper.go:94-96
+  if (axis_index >= 2 * k)  // nmt_wrapper.go:94-96 (no uint32 wrap at 0xFFFFFFFF)
     return fail(ctx, CEL_EPUSHPAST, "pushed past predetermined square size: boundary at " + std::to_string(2 * k) +
                                         " index at " + std::to_string(axis_index) + " 0");
   if (flags & CEL_FLAG_ORDER_CHECK) {
@@ -205,7 +205,7 @@ cel_status cel_axis_tree(cel_ctx* ctx, const uint8_t* cells, uint32_t k, uint32_
   if (!cells || !nodes_out) return fail(ctx, CEL_EINVAL, "nil argument");
   cel_status st = validate_square(ctx, k, share_size);
   if (st) return st;
-  if (axis_index + 1 > 2 * k)  // nmt_wrapper.go:94-96
+  if (axis_index >= 2 * k)  // nmt_wrapper.go:94-96 (no uint32 wrap at 0xFFFFFFFF)
     return fail(ctx, CEL_EPUSHPAST, "pushed past predetermined square size: boundary at " + std::to_string(2 * k) +
                                         " index at " + std::to_string(axis_index) + " 0");
   std::vector<uint8_t> dense(cells, cells + (size_t)2 * k * kShare);

@@ -150,7 +150,7 @@ hipError_t launch_shard_finish(const uint32_t* gathered, uint32_t k, uint32_t nr
 // Same-run probes (probe_kernels.hip): SHA-256 chained in registers (out: blocks*256 words,
 // clk: 2 counters per wave), and a streaming copy of `bytes` (a multiple of 16).
 hipError_t launch_probe_sha(uint32_t* out, unsigned long long* clk, uint32_t blocks, int n, hipStream_t s);
-hipError_t launch_probe_copy(const void* src, void* dst, uint64_t bytes, uint32_t blocks, hipStream_t s);
+hipError_t launch_probe_copy(const void* src, void* dst, uint64_t bytes, uint32_t blocks, bool nt, hipStream_t s);
 
 // Repair helpers (repair_kernels.hip, nmt_kernels.hip).
 hipError_t launch_gather_axes(const uint8_t* eds, const uint8_t* mask, uint32_t W, const int32_t* idx, int is_col,

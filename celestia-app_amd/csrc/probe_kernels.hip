@@ -7,8 +7,9 @@
 //                 the shader-clock counter (s_memtime) and the constant-rate counter
 //                 (s_memrealtime) at its start and end, so the sustained clock under a
 //                 VALU-bound load comes from the same launch.
-//   k_probe_copy  a streaming copy (dwordx4, non-temporal like the RS kernels' accesses):
-//                 achievable HBM bytes/s, read + write.
+//   k_probe_copy  a streaming copy (16 KiB chunks per workgroup, four dwordx4 loads in
+//                 flight per lane, non-temporal or default policy): achievable HBM bytes/s,
+//                 read + write.
 #include <hip/hip_runtime.h>
 
 #include "cel_internal.hpp"
@@ -43,12 +44,30 @@ __global__ __launch_bounds__(256, 4) void k_probe_sha(uint32_t* out, unsigned lo
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// Each workgroup copies contiguous 16 KiB chunks (four dwordx4 loads in flight per lane
+// before their stores), chunk index grid-strided: the fastest shape of the sweep in
+// tools/microbench/hbm_copy.hip (profiles/r5_hbm_copy_sweep.txt: 5.6-5.8 TB/s non-temporal
+// at 4-16 workgroups per CU, against 4.6-5.5 for grid-strided lanes). NT = non-temporal.
+template <bool NT>
 __global__ __launch_bounds__(256) void k_probe_copy(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
                                                     uint64_t n16) {
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
-    const u32x4 v = __builtin_nontemporal_load(src + i);
-    __builtin_nontemporal_store(v, dst + i);
+  constexpr uint64_t kPer = 256 * 4;
+  for (uint64_t c = blockIdx.x; c * kPer < n16; c += gridDim.x) {
+    const uint64_t b = c * kPer + threadIdx.x;
+    if (b + 3 * 256 < n16) {
+      u32x4 v[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) v[j] = NT ? __builtin_nontemporal_load(src + b + j * 256) : src[b + j * 256];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        if (NT)
+          __builtin_nontemporal_store(v[j], dst + b + j * 256);
+        else
+          dst[b + j * 256] = v[j];
+      }
+    } else {
+      for (uint64_t i = b; i < n16 && i < c * kPer + kPer; i += 256) dst[i] = src[i];
+    }
   }
 }
 
@@ -57,9 +76,13 @@ hipError_t launch_probe_sha(uint32_t* out, unsigned long long* clk, uint32_t blo
   return hipGetLastError();
 }
 
-hipError_t launch_probe_copy(const void* src, void* dst, uint64_t bytes, uint32_t blocks, hipStream_t s) {
-  hipLaunchKernelGGL(k_probe_copy, dim3(blocks), dim3(256), 0, s, static_cast<const u32x4*>(src),
-                     static_cast<u32x4*>(dst), bytes / 16);
+hipError_t launch_probe_copy(const void* src, void* dst, uint64_t bytes, uint32_t blocks, bool nt, hipStream_t s) {
+  if (nt)
+    hipLaunchKernelGGL(k_probe_copy<true>, dim3(blocks), dim3(256), 0, s, static_cast<const u32x4*>(src),
+                       static_cast<u32x4*>(dst), bytes / 16);
+  else
+    hipLaunchKernelGGL(k_probe_copy<false>, dim3(blocks), dim3(256), 0, s, static_cast<const u32x4*>(src),
+                       static_cast<u32x4*>(dst), bytes / 16);
   return hipGetLastError();
 }
 

@@ -446,6 +446,11 @@ func (c *Context) GetCommitment(eds []byte, k, start, blobShareLen, subtreeRootT
 // nmt.NewInclusionProof(start, end, nodes, true) turns into the nmt.Proof the wrapper
 // returns (IgnoreMaxNamespace, as wrapper.NewErasuredNamespacedMerkleTree sets it).
 func (c *Context) ProveRange(cells [][]byte, k, axisIndex, start, end int) ([][]byte, error) {
+	// Go ints would wrap through C.uint32_t: reject what the reference tree would never see
+	if k <= 0 || axisIndex < 0 || axisIndex >= 2*k || start < 0 || end < 0 {
+		return nil, &StatusError{Status: int(C.CEL_EINVAL),
+			Msg: fmt.Sprintf("invalid ProveRange arguments: k=%d axisIndex=%d range [%d, %d)", k, axisIndex, start, end)}
+	}
 	if len(cells) != 2*k || !deviceShares(cells) {
 		return nil, &StatusError{Status: int(C.CEL_EINVAL), Msg: "ProveRange needs the axis's 2k shares of 512 bytes"}
 	}

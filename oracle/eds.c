@@ -425,6 +425,17 @@ static uint8_t* thread_scratch(size_t bytes) {
   return tl_buf;
 }
 
+/* End of a call: a thread keeps its scratch only up to a k=128 square's size, so a k=512
+ * repair's ~0.5 GiB per thread is not held by the process after the call. */
+#define ORC_SCRATCH_KEEP ((size_t)64 << 20)
+static void thread_scratch_trim(void) {
+  if (tl_cap > ORC_SCRATCH_KEEP) {
+    free(tl_buf);
+    tl_buf = NULL;
+    tl_cap = 0;
+  }
+}
+
 int orc_extend_commit_many(const uint8_t* ods, uint32_t n, uint32_t k, size_t share, uint8_t* dah_out) {
   orc_init();
   const size_t ods_b = (size_t)k * k * share, eds_b = 4 * ods_b, roots_b = (size_t)2 * k * ORC_NODE;
@@ -436,15 +447,16 @@ int orc_extend_commit_many(const uint8_t* ods, uint32_t n, uint32_t k, size_t sh
 #pragma omp parallel reduction(| : rc)
   {
     uint8_t* eds = thread_scratch(eds_b + 2 * roots_b);
-    uint8_t* rr = eds + eds_b;
-    uint8_t* cr = rr + roots_b;
+    uint8_t* rr = eds ? eds + eds_b : NULL;
+    uint8_t* cr = rr ? rr + roots_b : NULL;
 #pragma omp for schedule(dynamic, 1)
     for (int64_t i = 0; i < (int64_t)n; i++) {
-      int r = orc_extend(ods + (size_t)i * ods_b, k, share, eds);
+      int r = eds ? orc_extend(ods + (size_t)i * ods_b, k, share, eds) : ORC_ENOMEM;
       if (r == ORC_OK) r = orc_roots(eds, k, share, rr, cr, 1, NULL);
       if (r == ORC_OK) orc_dah_hash(rr, cr, 2 * k, dah_out + (size_t)i * 32);
       rc |= r;
     }
+    thread_scratch_trim();
   }
 #ifdef _OPENMP
   omp_set_max_active_levels(levels);
@@ -459,13 +471,18 @@ int orc_repair_many(const uint8_t* eds, const uint8_t* present, uint32_t k, size
 #pragma omp parallel
   {
     uint8_t* e = thread_scratch(eds_b + cells);
-    uint8_t* p = e + eds_b;
+    uint8_t* p = e ? e + eds_b : NULL;
 #pragma omp for schedule(dynamic, 1)
     for (int64_t i = 0; i < (int64_t)n; i++) {
+      if (!e) {
+        status_out[i] = ORC_ENOMEM;
+        continue;
+      }
       memcpy(e, eds, eds_b);
       memcpy(p, present, cells);
       status_out[i] = orc_repair(e, p, k, share, row_roots, col_roots, NULL, NULL, NULL, NULL);
     }
+    thread_scratch_trim();
   }
   return ORC_OK;
 }

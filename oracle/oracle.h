@@ -40,6 +40,7 @@ extern "C" {
 #define ORC_ETOOFEW 6
 #define ORC_EBYZANTINE 7
 #define ORC_EUNREPAIRABLE 8
+#define ORC_ENOMEM 10  /* host allocation failed (CPU baseline scratch) */
 #define ORC_EBADROOT 13 /* rsmt2d preRepairSanityCheck "bad root input" (not ErrByzantineData) */
 
 #define ORC_NS 29
