@@ -283,6 +283,89 @@ cel_status cel_dev_extend_batch(cel_ctx* ctx, const void* d_ods, uint32_t n, uin
   return e == hipSuccess ? CEL_OK : hip_fail(ctx, e, "extend batch");
 }
 
+static cel_status order_status(cel_ctx* ctx, int32_t st) {
+  if (st == CEL_EORDER) return fail(ctx, CEL_EORDER, "invalid push order: leaf namespaces must be non-decreasing");
+  return st;
+}
+
+// Device address of host memory the GPU can read directly (page-locked: cel_host_alloc,
+// hipHostMalloc / hipHostRegister), or nullptr for pageable memory.
+static const uint8_t* mapped_host(const uint8_t* p) {
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();  // clear the sticky "invalid value" of a pageable pointer
+    return nullptr;
+  }
+  if (at.type != hipMemoryTypeHost || !at.devicePointer || !at.hostPointer) return nullptr;
+  return static_cast<const uint8_t*>(at.devicePointer) + (p - static_cast<const uint8_t*>(at.hostPointer));
+}
+
+// One square from host buffers, latency first: PrepareProposal and ProcessProposal extend
+// one block at a time and keep only the header (app/prepare_proposal.go:61-92,
+// app/process_proposal.go:138-156). Everything on one stream, so nothing waits on another
+// queue (round 5: row chunks uploaded on a copy stream with the row passes waiting on
+// their events serialized behind the whole upload, profiles/r5_header_host_timeline.txt):
+//   - page-locked ODS: the row pass reads it straight from host memory over PCIe and
+//     writes Q0 and Q1 (the upload and the row transform are one launch);
+//     pageable ODS: one contiguous copy to the device first, then the row pass;
+//   - the column pass, every leaf, the tree levels and the DAH;
+//   - every result in one copy into page-locked staging (separate copies into pageable
+//     memory cost a staging kernel and a host wait each).
+// The EDS download, if asked for, runs on a download stream after the column pass.
+static cel_status extend_one(cel_ctx* ctx, const uint8_t* ods, uint32_t k, uint8_t* eds_out, uint8_t* row_roots,
+                             uint8_t* col_roots, uint8_t* dah, int32_t* status_out, uint32_t flags) {
+  const size_t ods_b = (size_t)k * k * kShare, eds_b = 4 * ods_b, roots_b = (size_t)2 * k * kNode;
+  const size_t out_b = 2 * roots_b + 32 + 4;
+  hipError_t e = hipSuccess;
+  const uint8_t* src = mapped_host(ods);
+  uint8_t* d_eds = static_cast<uint8_t*>(scratch(ctx, S_EDS, eds_b, &e));
+  uint8_t* d_ods = src ? nullptr : static_cast<uint8_t*>(scratch(ctx, S_IN, ods_b, &e));
+  uint8_t* d_work = static_cast<uint8_t*>(scratch(ctx, S_WORK, nmt_workspace_size(k, 1), &e));
+  uint8_t* d_out = static_cast<uint8_t*>(scratch(ctx, S_ROOTS, out_b, &e));
+  uint8_t* h_out = static_cast<uint8_t*>(host_stage(ctx, out_b));
+  if (!d_eds || (!src && !d_ods) || !d_work || !d_out || !h_out) return fail(ctx, CEL_ENOMEM, "allocation failed");
+  int32_t* d_st = reinterpret_cast<int32_t*>(d_out + 2 * roots_b + 32);
+  hipStream_t s = ctx->stream, d = ctx->dl[0];
+  auto enqueue = [&]() -> hipError_t {
+    hipError_t r;
+    if (!src) {
+      if ((r = hipMemcpyAsync(d_ods, ods, ods_b, hipMemcpyHostToDevice, s)) != hipSuccess) return r;
+      src = d_ods;
+    }
+    if ((r = launch_extend_rows(d_eds, k, 0, k, ctx->tables, s, src)) != hipSuccess ||
+        (r = launch_extend_cols(d_eds, k, 1, ctx->tables, s)) != hipSuccess)
+      return r;
+    if (eds_out &&
+        ((r = hipEventRecord(ctx->ev_rs[0], s)) != hipSuccess || (r = hipStreamWaitEvent(d, ctx->ev_rs[0], 0))))
+      return r;
+    if ((r = launch_commit(d_eds, k, 1, d_out, d_out + roots_b, d_out + 2 * roots_b, d_st, d_work,
+                           (flags & CEL_FLAG_ORDER_CHECK) != 0, s)) != hipSuccess ||
+        (r = hipMemcpyAsync(h_out, d_out, out_b, hipMemcpyDeviceToHost, s)) != hipSuccess)
+      return r;
+    if (eds_out) {
+      // after every kernel is enqueued: a copy into pageable memory blocks the calling thread
+      const size_t rowb = (size_t)2 * k * kShare, half = (size_t)k * kShare;
+      r = (flags & CEL_FLAG_PARITY_ONLY)
+              ? hipMemcpy2DAsync(eds_out + half, rowb, d_eds + half, rowb, half, k, hipMemcpyDeviceToHost, d)
+              : hipMemcpyAsync(eds_out, d_eds, k * rowb, hipMemcpyDeviceToHost, d);
+      if (r == hipSuccess)
+        r = hipMemcpyAsync(eds_out + k * rowb, d_eds + k * rowb, k * rowb, hipMemcpyDeviceToHost, d);
+      if (r == hipSuccess) r = hipEventRecord(ctx->ev_dl[0], d);
+      if (r == hipSuccess) r = hipStreamWaitEvent(s, ctx->ev_dl[0], 0);
+    }
+    return r;
+  };
+  if ((e = enqueue()) != hipSuccess) return hip_fail(ctx, e, "extend square");
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "sync");
+  std::memcpy(row_roots, h_out, roots_b);
+  std::memcpy(col_roots, h_out + roots_b, roots_b);
+  std::memcpy(dah, h_out + 2 * roots_b, 32);
+  int32_t stv = 0;
+  std::memcpy(&stv, h_out + 2 * roots_b + 32, 4);
+  if (status_out) *status_out = stv;
+  return order_status(ctx, stv);
+}
+
 cel_status cel_extend_batch(cel_ctx* ctx, const uint8_t* ods, uint32_t n, uint32_t k, uint32_t share_size,
                             uint8_t* eds_out, uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah,
                             int32_t* status_out, uint32_t flags) {
@@ -292,6 +375,7 @@ cel_status cel_extend_batch(cel_ctx* ctx, const uint8_t* ods, uint32_t n, uint32
   cel_status st = validate_square(ctx, k, share_size);
   if (st) return st;
   DeviceGuard g(ctx->device);
+  if (n == 1 && k >= 32) return extend_one(ctx, ods, k, eds_out, row_roots, col_roots, dah, status_out, flags);
   const size_t ods_b = (size_t)n * k * k * kShare, eds_b = 4 * ods_b;
   const size_t roots_b = (size_t)n * 2 * k * kNode;
   hipError_t e = hipSuccess;
@@ -309,8 +393,11 @@ cel_status cel_extend_batch(cel_ctx* ctx, const uint8_t* ods, uint32_t n, uint32
   if (!d_eds) return fail(ctx, CEL_ENOMEM, "device allocation failed");
   uint8_t* d_work = static_cast<uint8_t*>(scratch(ctx, S_WORK, nstreams * ws, &e));
   if (!d_work) return fail(ctx, CEL_ENOMEM, "device allocation failed");
-  uint8_t* d_out = static_cast<uint8_t*>(scratch(ctx, S_ROOTS, 2 * roots_b + (size_t)n * 32 + (size_t)n * 4, &e));
+  const size_t out_b = 2 * roots_b + (size_t)n * 32 + (size_t)n * 4;
+  uint8_t* d_out = static_cast<uint8_t*>(scratch(ctx, S_ROOTS, out_b, &e));
   if (!d_out) return fail(ctx, CEL_ENOMEM, "device allocation failed");
+  uint8_t* h_out = static_cast<uint8_t*>(host_stage(ctx, out_b));
+  if (!h_out) return fail(ctx, CEL_ENOMEM, "page-locked allocation failed");
   uint8_t* d_rr = d_out;
   uint8_t* d_cr = d_out + roots_b;
   uint8_t* d_dah = d_out + 2 * roots_b;
@@ -339,7 +426,9 @@ cel_status cel_extend_batch(cel_ctx* ctx, const uint8_t* ods, uint32_t n, uint32
     const uint32_t first = c * chunk, cnt = (first + chunk <= n) ? chunk : n - first;
     hipStream_t cs = ctx->sub[c % cel_ctx::kPipe];
     uint8_t* eds_c = d_eds + first * eds_sq;
-    hipStream_t ds = ctx->dl[c % cel_ctx::kPipe];
+    // one download stream, chunks in order: one DMA stream at the link's rate (four
+    // concurrent ones measured 1.75K -> 1.0K squares/s on the parity-only copies)
+    hipStream_t ds = ctx->dl[0];
     if (eds_out && (e = hipStreamWaitEvent(ds, ctx->ev_rs[c % cel_ctx::kChunks], 0)) != hipSuccess)
       return hip_fail(ctx, e, "event");
     if (eds_out && (flags & CEL_FLAG_PARITY_ONLY)) {
@@ -357,31 +446,27 @@ cel_status cel_extend_batch(cel_ctx* ctx, const uint8_t* ods, uint32_t n, uint32
                                               ds)) != hipSuccess) {
       return hip_fail(ctx, e, "D2H");
     }
-    if ((e = hipMemcpyAsync(row_roots + first * roots_sq, d_rr + first * roots_sq, cnt * roots_sq,
-                            hipMemcpyDeviceToHost, cs)) != hipSuccess ||
-        (e = hipMemcpyAsync(col_roots + first * roots_sq, d_cr + first * roots_sq, cnt * roots_sq,
-                            hipMemcpyDeviceToHost, cs)) != hipSuccess ||
-        (e = hipMemcpyAsync(dah + first * 32, d_dah + first * 32, (size_t)cnt * 32, hipMemcpyDeviceToHost, cs)) !=
-            hipSuccess ||
-        (e = hipMemcpyAsync(stv.data() + first, d_st + first, (size_t)cnt * 4, hipMemcpyDeviceToHost, cs)) !=
-            hipSuccess)
-      return hip_fail(ctx, e, "D2H");
     if ((e = hipEventRecord(ctx->ev_done[c % cel_ctx::kChunks], cs)) != hipSuccess ||
         (e = hipStreamWaitEvent(s, ctx->ev_done[c % cel_ctx::kChunks], 0)) != hipSuccess)
       return hip_fail(ctx, e, "event");
   }
-  for (uint32_t i = 0; eds_out && i < nstreams; i++)
-    if ((e = hipEventRecord(ctx->ev_dl[i], ctx->dl[i])) != hipSuccess ||
-        (e = hipStreamWaitEvent(s, ctx->ev_dl[i], 0)) != hipSuccess)
-      return hip_fail(ctx, e, "event");
+  if (eds_out && ((e = hipEventRecord(ctx->ev_dl[0], ctx->dl[0])) != hipSuccess ||
+                  (e = hipStreamWaitEvent(s, ctx->ev_dl[0], 0)) != hipSuccess))
+    return hip_fail(ctx, e, "event");
+  // every result in one copy into page-locked staging (one D2H into pageable memory costs
+  // a staging kernel and a host wait each: four of them per chunk were ~25 us apiece)
+  if ((e = hipMemcpyAsync(h_out, d_out, out_b, hipMemcpyDeviceToHost, s)) != hipSuccess) return hip_fail(ctx, e, "D2H");
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "sync");
+  std::memcpy(row_roots, h_out, roots_b);
+  std::memcpy(col_roots, h_out + roots_b, roots_b);
+  std::memcpy(dah, h_out + 2 * roots_b, (size_t)n * 32);
+  std::memcpy(stv.data(), h_out + 2 * roots_b + (size_t)n * 32, (size_t)n * 4);
   cel_status worst = CEL_OK;
   for (uint32_t i = 0; i < n; i++) {
     if (status_out) status_out[i] = stv[i];
     if (stv[i] != CEL_OK && worst == CEL_OK) worst = stv[i];
   }
-  if (worst == CEL_EORDER) return fail(ctx, CEL_EORDER, "invalid push order: leaf namespaces must be non-decreasing");
-  return worst;
+  return order_status(ctx, worst);
 }
 
 cel_status cel_extend_shares(cel_ctx* ctx, const uint8_t* shares, uint32_t n_shares, uint32_t share_size,

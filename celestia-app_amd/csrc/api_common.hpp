@@ -36,6 +36,19 @@ inline void* scratch(cel_ctx* ctx, int slot, size_t bytes, hipError_t* err) {
   return p;
 }
 
+// Grow-only page-locked host staging of a ctx (calls on a ctx hold its lock, so one buffer
+// serves them all): device results come back in one asynchronous copy into it, then a host
+// memcpy to the caller's (often pageable) buffers. nullptr if the allocation fails.
+inline void* host_stage(cel_ctx* ctx, size_t bytes) {
+  if (ctx->hstage_size >= bytes) return ctx->hstage;
+  if (ctx->hstage) (void)hipHostFree(ctx->hstage);
+  ctx->hstage = nullptr;
+  ctx->hstage_size = 0;
+  if (hipHostMalloc(&ctx->hstage, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+  ctx->hstage_size = bytes;
+  return ctx->hstage;
+}
+
 inline bool is_pow2(uint64_t n) { return n && !(n & (n - 1)); }
 
 // da.SquareSize: RoundUpPowerOfTwo(ceil(sqrt(len))) (data_availability_header.go:205-215)

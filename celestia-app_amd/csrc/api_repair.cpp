@@ -847,14 +847,7 @@ static cel_status repair_bufs(cel_ctx* ctx, uint32_t k, bool own_eds, RepairBufs
   const size_t cells_h = (cells + 255) & ~(size_t)255;
   // axis lists, mask + first list, results
   const size_t hb = (size_t)kIdxSlots * W * 4 + cells_h + list_a + b->res_bytes;
-  if (ctx->hstage_size < hb) {
-    if (ctx->hstage) (void)hipHostFree(ctx->hstage);
-    ctx->hstage = nullptr;
-    ctx->hstage_size = 0;
-    if (hipHostMalloc(&ctx->hstage, hb, hipHostMallocDefault) != hipSuccess)
-      return fail(ctx, CEL_ENOMEM, "page-locked allocation failed");
-    ctx->hstage_size = hb;
-  }
+  if (!host_stage(ctx, hb)) return fail(ctx, CEL_ENOMEM, "page-locked allocation failed");
   b->hidx = static_cast<int32_t*>(ctx->hstage);
   b->hmask = static_cast<uint8_t*>(ctx->hstage) + (size_t)kIdxSlots * W * 4;
   b->hres = b->hmask + cells_h + list_a;

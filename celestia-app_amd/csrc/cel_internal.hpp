@@ -103,12 +103,25 @@ hipError_t launch_rs_encode_gf16x(const RsGeom& g, hipStream_t s);     // GF(2^1
 // ods == nullptr means Q0 is already in place inside eds.
 hipError_t launch_extend(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t nsq,
                          const DeviceTables& t, hipStream_t s);
+// The two passes apart, for one square's latency path: Q0 rows [row0, row1) -> Q1 (Q0
+// read in place in the EDS, or from a contiguous k x k ODS `ods` and then also written into
+// Q0), and all 2k columns -> Q2|Q3 of nsq squares.
+hipError_t launch_extend_rows(uint8_t* eds, uint32_t k, uint32_t row0, uint32_t row1, const DeviceTables& t,
+                              hipStream_t s, const uint8_t* ods = nullptr);
+hipError_t launch_extend_cols(uint8_t* eds, uint32_t k, uint32_t nsq, const DeviceTables& t, hipStream_t s);
 
 // NMT + DAH over resident EDSs. work: scratch of nmt_workspace_size(k, nsq) bytes.
 size_t nmt_workspace_size(uint32_t k, uint32_t nsq);
 hipError_t launch_commit(const uint8_t* eds, uint32_t k, uint32_t nsq, uint8_t* row_roots,
                          uint8_t* col_roots, uint8_t* dah, int32_t* status, void* work,
                          bool order_check, hipStream_t s);
+// The same commit in two steps: the leaves of EDS rows [row0, row1) of every square
+// (init_bad: reset the push-order flags first; it must precede every leaf launch of the
+// commit in stream order), then, after every leaf, the tree levels, roots and DAH.
+hipError_t launch_commit_leaves(const uint8_t* eds, uint32_t k, uint32_t nsq, void* work, bool order_check,
+                                uint32_t row0, uint32_t row1, bool init_bad, hipStream_t s);
+hipError_t launch_commit_trees(uint32_t k, uint32_t nsq, uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah,
+                               int32_t* status, void* work, hipStream_t s);
 // One erasured axis root (cells contiguous) or plain NMT root over leaves.
 hipError_t launch_axis_root(const uint8_t* cells, uint32_t k, uint32_t axis, uint8_t* root,
                             void* work, hipStream_t s);

@@ -194,13 +194,14 @@ __device__ __forceinline__ void make_leaf_node(const uint32_t* __restrict__ sh, 
   put_digest(nd, st);
 }
 
-// grid: x = cell block (256 cells), y = square. Writes leaf nodes [sq][W*W][24].
+// grid: x = cell block (256 cells from cell0), y = square. Writes leaf nodes [sq][W*W][24]
+// of cells [cell0, cell1).
 template <bool ORDER, bool PF>
 __global__ __launch_bounds__(256) void k_leaf(const uint8_t* __restrict__ eds, uint32_t k, uint32_t* __restrict__ leaves,
-                                              int32_t* __restrict__ bad_axis) {
+                                              int32_t* __restrict__ bad_axis, uint32_t cell0, uint32_t cell1) {
   const uint32_t W = 2 * k;
-  const uint32_t cell = blockIdx.x * 256u + threadIdx.x;
-  if (cell >= W * W) return;
+  const uint32_t cell = cell0 + blockIdx.x * 256u + threadIdx.x;
+  if (cell >= cell1) return;
   const uint32_t r = cell / W, c = cell % W;
   const uint64_t sq_eds = (uint64_t)W * W * kShare;
   const uint32_t* sh = reinterpret_cast<const uint32_t*>(eds + blockIdx.y * sq_eds + (uint64_t)cell * kShare);
@@ -502,48 +503,65 @@ size_t nmt_workspace_size(uint32_t k, uint32_t nsq) {
          align256(nsq * 2 * W * 32);
 }
 
-hipError_t launch_commit(const uint8_t* eds, uint32_t k, uint32_t nsq, uint8_t* row_roots, uint8_t* col_roots,
-                         uint8_t* dah, int32_t* status, void* work, bool order_check, hipStream_t s) {
+struct CommitWork {
+  uint32_t *leaves, *ping, *pong, *roots, *leafd;
+  int32_t* bad;
+};
+
+static CommitWork commit_work(void* work, uint32_t k, uint32_t nsq) {
   const uint32_t W = 2 * k;
   const size_t nb = kNodeWords * 4;
   uint8_t* base = static_cast<uint8_t*>(work);
-  uint32_t* leaves = reinterpret_cast<uint32_t*>(base);
+  CommitWork w;
+  w.leaves = reinterpret_cast<uint32_t*>(base);
   base += align256((size_t)nsq * W * W * nb);
-  uint32_t* ping = reinterpret_cast<uint32_t*>(base);
+  w.ping = reinterpret_cast<uint32_t*>(base);
   base += align256((size_t)nsq * 2 * W * (W / 2 + 1) * nb);
-  uint32_t* pong = reinterpret_cast<uint32_t*>(base);
+  w.pong = reinterpret_cast<uint32_t*>(base);
   base += align256((size_t)nsq * 2 * W * (W / 4 + 1) * nb);
-  uint32_t* roots = reinterpret_cast<uint32_t*>(base);
+  w.roots = reinterpret_cast<uint32_t*>(base);
   base += align256((size_t)nsq * 2 * W * nb);
-  int32_t* bad = reinterpret_cast<int32_t*>(base);
+  w.bad = reinterpret_cast<int32_t*>(base);
   base += align256((size_t)nsq * 4 + 4);
-  uint32_t* leafd = reinterpret_cast<uint32_t*>(base);
+  w.leafd = reinterpret_cast<uint32_t*>(base);
+  return w;
+}
 
-  {
-    const Range r("nmt.leaf");
-    hipLaunchKernelGGL(k_fill_i32, dim3((nsq + 255) / 256), dim3(256), 0, s, bad, nsq, INT_MAX);
-    dim3 gl((W * W + 255) / 256, nsq);
-    if (latency_bound(W * W * nsq)) {
-      if (order_check) hipLaunchKernelGGL((k_leaf<true, true>), gl, dim3(256), 0, s, eds, k, leaves, bad);
-      else hipLaunchKernelGGL((k_leaf<false, true>), gl, dim3(256), 0, s, eds, k, leaves, bad);
-    } else {
-      if (order_check) hipLaunchKernelGGL((k_leaf<true, false>), gl, dim3(256), 0, s, eds, k, leaves, bad);
-      else hipLaunchKernelGGL((k_leaf<false, false>), gl, dim3(256), 0, s, eds, k, leaves, bad);
-    }
+hipError_t launch_commit_leaves(const uint8_t* eds, uint32_t k, uint32_t nsq, void* work, bool order_check,
+                                uint32_t row0, uint32_t row1, bool init_bad, hipStream_t s) {
+  const uint32_t W = 2 * k;
+  const CommitWork w = commit_work(work, k, nsq);
+  const Range r("nmt.leaf");
+  if (init_bad) hipLaunchKernelGGL(k_fill_i32, dim3((nsq + 255) / 256), dim3(256), 0, s, w.bad, nsq, INT_MAX);
+  const uint32_t c0 = row0 * W, c1 = row1 * W;
+  if (c1 <= c0) return hipGetLastError();
+  dim3 gl((c1 - c0 + 255) / 256, nsq);
+  if (latency_bound((uint64_t)(c1 - c0) * nsq)) {
+    if (order_check) hipLaunchKernelGGL((k_leaf<true, true>), gl, dim3(256), 0, s, eds, k, w.leaves, w.bad, c0, c1);
+    else hipLaunchKernelGGL((k_leaf<false, true>), gl, dim3(256), 0, s, eds, k, w.leaves, w.bad, c0, c1);
+  } else {
+    if (order_check) hipLaunchKernelGGL((k_leaf<true, false>), gl, dim3(256), 0, s, eds, k, w.leaves, w.bad, c0, c1);
+    else hipLaunchKernelGGL((k_leaf<false, false>), gl, dim3(256), 0, s, eds, k, w.leaves, w.bad, c0, c1);
   }
+  return hipGetLastError();
+}
 
+hipError_t launch_commit_trees(uint32_t k, uint32_t nsq, uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah,
+                               int32_t* status, void* work, hipStream_t s) {
+  const uint32_t W = 2 * k;
+  const CommitWork w = commit_work(work, k, nsq);
   // One launch per tree level, all 4k trees of all squares at once: every lane hashes
   // one node, no idle lanes. The last level writes the root records.
   const uint32_t trees = 2 * W;
   uint32_t nin = W;
-  const uint32_t* src = leaves;
-  uint32_t* dst = ping;
+  const uint32_t* src = w.leaves;
+  uint32_t* dst = w.ping;
   bool first = true;
   roctxRangePushA("nmt.levels");
   while (nin > 1) {
     const uint32_t nout = nin / 2;
-    uint32_t* out = (nout == 1) ? roots : dst;
-    uint32_t* ld = (nout == 1 && dah) ? leafd : nullptr;  // dah == nullptr: roots only
+    uint32_t* out = (nout == 1) ? w.roots : dst;
+    uint32_t* ld = (nout == 1 && dah) ? w.leafd : nullptr;  // dah == nullptr: roots only
     dim3 g((trees * nout + 255) / 256, nsq);
     uint8_t* ro = (nout == 1) ? row_roots : nullptr;
     uint8_t* co = (nout == 1) ? col_roots : nullptr;
@@ -551,7 +569,7 @@ hipError_t launch_commit(const uint8_t* eds, uint32_t k, uint32_t nsq, uint8_t* 
     else hipLaunchKernelGGL(k_level<false>, g, dim3(256), 0, s, src, out, W, nin, trees, ld, ro, co);
     first = false;
     src = out;
-    dst = (dst == ping) ? pong : ping;
+    dst = (dst == w.ping) ? w.pong : w.ping;
     nin = nout;
   }
   roctxRangePop();
@@ -559,9 +577,16 @@ hipError_t launch_commit(const uint8_t* eds, uint32_t k, uint32_t nsq, uint8_t* 
   // roots already packed into row_roots / col_roots by the root level
   const Range r("dah");
   if (dah)
-    hipLaunchKernelGGL(k_merkle, dim3(nsq), dim3(merkle_block(trees)), lds, s, roots, leafd, trees, dah, nullptr,
-                       nullptr, bad, status);
+    hipLaunchKernelGGL(k_merkle, dim3(nsq), dim3(merkle_block(trees)), lds, s, w.roots, w.leafd, trees, dah, nullptr,
+                       nullptr, w.bad, status);
   return hipGetLastError();
+}
+
+hipError_t launch_commit(const uint8_t* eds, uint32_t k, uint32_t nsq, uint8_t* row_roots, uint8_t* col_roots,
+                         uint8_t* dah, int32_t* status, void* work, bool order_check, hipStream_t s) {
+  hipError_t e = launch_commit_leaves(eds, k, nsq, work, order_check, 0, 2 * k, true, s);
+  if (e == hipSuccess) e = launch_commit_trees(k, nsq, row_roots, col_roots, dah, status, work, s);
+  return e;
 }
 
 

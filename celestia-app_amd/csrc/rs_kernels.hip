@@ -233,33 +233,53 @@ static RsGeom row_geom(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t ns
   return r;
 }
 
-hipError_t launch_extend(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t nsq, const DeviceTables& t,
-                         hipStream_t s) {
-  if (nsq == 0) return hipSuccess;
+// columns of [Q0|Q1] -> [Q2|Q3] (all 2k columns, after every row)
+static RsGeom col_geom(uint8_t* eds, uint32_t k, uint32_t nsq) {
   const uint64_t row = (uint64_t)2 * k * kShare;  // bytes per EDS row
-  const uint64_t sq_eds = (uint64_t)4 * k * k * kShare;
-  hipError_t e;
-  // Q0 rows -> Q1 (reading the ODS and writing Q0 into the EDS on the way when ods != nullptr)
-  {
-    const Range r("rs.rows");
-    if ((e = launch_rs_encode(row_geom(ods, eds, k, nsq), t, s)) != hipSuccess) return e;
-  }
-  // columns of [Q0|Q1] -> [Q2|Q3]
   RsGeom cols{};
   cols.in = eds;
-  cols.in_sq = sq_eds;
+  cols.in_sq = (uint64_t)4 * k * k * kShare;
   cols.in_axis = kShare;
   cols.in_shard = row;
   cols.out = eds + (uint64_t)k * row;
-  cols.out_sq = sq_eds;
+  cols.out_sq = cols.in_sq;
   cols.out_axis = kShare;
   cols.out_shard = row;
   cols.n = k;
   cols.len = kShare;
   cols.axes = 2 * k;
   cols.nsq = nsq;
+  return cols;
+}
+
+hipError_t launch_extend(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t nsq, const DeviceTables& t,
+                         hipStream_t s) {
+  if (nsq == 0) return hipSuccess;
+  hipError_t e;
+  // Q0 rows -> Q1 (reading the ODS and writing Q0 into the EDS on the way when ods != nullptr)
+  {
+    const Range r("rs.rows");
+    if ((e = launch_rs_encode(row_geom(ods, eds, k, nsq), t, s)) != hipSuccess) return e;
+  }
   const Range r("rs.cols");
-  return launch_rs_encode(cols, t, s);
+  return launch_rs_encode(col_geom(eds, k, nsq), t, s);
+}
+
+hipError_t launch_extend_rows(uint8_t* eds, uint32_t k, uint32_t row0, uint32_t row1, const DeviceTables& t,
+                              hipStream_t s, const uint8_t* ods) {
+  RsGeom g = row_geom(ods, eds, k, 1);
+  const uint64_t off = (uint64_t)row0 * 2 * k * kShare;
+  g.in += ods ? (uint64_t)row0 * k * kShare : off;
+  if (ods) g.dcopy += off;
+  g.out += off;
+  g.axes = row1 - row0;
+  const Range r("rs.rows");
+  return launch_rs_encode(g, t, s);
+}
+
+hipError_t launch_extend_cols(uint8_t* eds, uint32_t k, uint32_t nsq, const DeviceTables& t, hipStream_t s) {
+  const Range r("rs.cols");
+  return launch_rs_encode(col_geom(eds, k, nsq), t, s);
 }
 
 // ------------------------------------------------------------------ decode

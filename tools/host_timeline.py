@@ -4,8 +4,9 @@ and --marker-trace (dev aid).
 python tools/host_timeline.py <dir> <marker> [before_us] [after_us] [which]
 
 Window: from `before_us` ahead of the start of occurrence `which` (default -1, the last)
-of roctx range `marker` to `after_us` past its end. Prints every kernel (K), HIP API
-call (H) and roctx range (M) in the window by start time: start offset and duration (us).
+of roctx range `marker` to `after_us` past its end. Prints every kernel (K), memory copy
+(C), HIP API call (H) and roctx range (M) in the window by start time: start offset and
+duration (us).
 """
 import csv
 import glob
@@ -28,6 +29,9 @@ ev = []
 for r in rows('*kernel_trace.csv'):
     ev.append((int(r['Start_Timestamp']), int(r['End_Timestamp']), 'K',
                r['Kernel_Name'].split('(')[0].replace('void ', '').replace('cel::', '')[:40]))
+for r in rows('*memory_copy_trace.csv'):
+    ev.append((int(r['Start_Timestamp']), int(r['End_Timestamp']), 'C',
+               (r.get('Direction', '') + ' ' + r.get('Size', '')).strip()[:40]))
 for r in rows('*hip_api_trace.csv'):
     ev.append((int(r['Start_Timestamp']), int(r['End_Timestamp']), 'H', r['Function'][:40]))
 marks = []
