@@ -18,7 +18,10 @@
 // RCCL refuses two ranks on one device ("Duplicate GPU detected", profiles/r3_rccl_probe.txt);
 // a plan whose ctxs repeat a device therefore moves the same blocks with device copies
 // (transport "copy", hipMemcpyPeerAsync) in the same schedule, which is how the plan's N > 1
-// schedule is tested on a one-GPU box. Distinct devices always use RCCL.
+// schedule is tested on a one-GPU box. Distinct devices always use RCCL. One rank needs no
+// collective (transport "local": the all-to-all is the identity, the row pass writes the slab
+// in place, and the gather is the rank's own record block) unless CEL_FLAG_SHARD_EXCHANGE asks
+// for the exchange through a one-rank RCCL communicator.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -87,7 +90,7 @@ const Rccl& rccl() {
 
 // One row-sharded square over ngpu devices: per-rank buffers, streams and communicators.
 struct cel_shard_plan {
-  enum Transport { kRccl, kCopy };
+  enum Transport { kRccl, kCopy, kLocal };
   struct Rank {
     int device = 0;
     hipStream_t s = nullptr;
@@ -96,7 +99,7 @@ struct cel_shard_plan {
     uint8_t* send = nullptr;      // [N][k/N][w][512] (the slab's top half when aliased)
     uint8_t* slab = nullptr;      // [2k][w][512]
     uint8_t* pack = nullptr;      // [2k + w + 1][96]: row subtrees, column roots, status record
-    uint8_t* gathered = nullptr;  // [N][2k + w + 1][96]
+    uint8_t* gathered = nullptr;  // [N][2k + w + 1][96] (the record block itself when local)
     uint8_t* work = nullptr;
     // rank 0: the finish's outputs, contiguous so one copy brings them back
     uint8_t* out = nullptr;  // row roots [2k][90] | col roots [2k][90] | dah [32] | status int32
@@ -142,8 +145,9 @@ void plan_free(cel_shard_plan* p) {
   for (size_t i = 0; i < p->r.size(); i++) {
     auto& rk = p->r[i];
     DeviceGuard g(rk.device);
-    for (uint8_t* b : {rk.ods_rows, rk.slab, rk.pack, rk.gathered, rk.work, rk.out})
+    for (uint8_t* b : {rk.ods_rows, rk.slab, rk.pack, rk.work, rk.out})
       if (b) (void)hipFree(b);
+    if (rk.gathered && rk.gathered != rk.pack) (void)hipFree(rk.gathered);
     if (rk.send && !p->alias) (void)hipFree(rk.send);
     free_tables(&rk.tables);
     for (hipEvent_t ev : {rk.ev_rows, rk.ev_exch, rk.ev_cols})
@@ -181,14 +185,15 @@ cel_status cel_shard_plan_create(cel_ctx* const* ctxs, uint32_t ngpu, uint32_t k
   p->k = k;
   p->w = 2 * k / ngpu;
   p->flags = flags;
-  p->alias = ngpu == 1 && !(flags & CEL_FLAG_SHARD_EXCHANGE);
+  p->alias = ngpu == 1 && !(flags & CEL_FLAG_SHARD_EXCHANGE);  // one rank, no collective
   p->r.resize(ngpu);
   std::vector<int> devs(ngpu);
   for (uint32_t i = 0; i < ngpu; i++) devs[i] = p->r[i].device = ctxs[i]->device;
   std::vector<int> sorted = devs;
   std::sort(sorted.begin(), sorted.end());
-  p->transport = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end() ? cel_shard_plan::kRccl
-                                                                                 : cel_shard_plan::kCopy;
+  p->transport = p->alias ? cel_shard_plan::kLocal
+                 : std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end() ? cel_shard_plan::kRccl
+                                                                                    : cel_shard_plan::kCopy;
   auto bail = [&](cel_status st, const std::string& msg) {
     c0->last_error = msg;
     plan_free(p);
@@ -205,7 +210,12 @@ cel_status cel_shard_plan_create(cel_ctx* const* ctxs, uint32_t ngpu, uint32_t k
     if (e == hipSuccess) e = hipMalloc(&rk.ods_rows, ods_b);
     if (e == hipSuccess) e = hipMalloc(&rk.slab, slab_b);
     if (e == hipSuccess) e = hipMalloc(&rk.pack, p->pack_bytes());
-    if (e == hipSuccess) e = hipMalloc(&rk.gathered, (size_t)ngpu * p->pack_bytes());
+    if (e == hipSuccess) {
+      if (p->alias)
+        rk.gathered = rk.pack;
+      else
+        e = hipMalloc(&rk.gathered, (size_t)ngpu * p->pack_bytes());
+    }
     if (e == hipSuccess) e = hipMalloc(&rk.work, work_b);
     if (e == hipSuccess) e = hipMemset(rk.pack, 0, p->pack_bytes());
     if (e == hipSuccess && i == 0) e = hipMalloc(&rk.out, p->out_bytes());
@@ -246,7 +256,7 @@ void cel_shard_plan_destroy(cel_shard_plan* plan) {
 
 const char* cel_shard_plan_transport(const cel_shard_plan* plan) {
   if (!plan) return "";
-  return plan->transport == cel_shard_plan::kRccl ? "rccl" : "copy";
+  return plan->transport == cel_shard_plan::kRccl ? "rccl" : plan->transport == cel_shard_plan::kCopy ? "copy" : "local";
 }
 
 const char* cel_shard_plan_last_error(const cel_shard_plan* plan) { return plan ? plan->last_error.c_str() : ""; }
@@ -329,7 +339,9 @@ cel_status cel_shard_plan_run(cel_shard_plan* p) {
   }
   // 4. gather every rank's record block (rank order)
   auto& r0 = p->r[0];
-  if (copy) {
+  if (p->transport == cel_shard_plan::kLocal) {
+    // one rank: its record block is the gathered block (finish reads it in place)
+  } else if (copy) {
     DeviceGuard g(r0.device);
     for (uint32_t r = 0; r < N && e == hipSuccess; r++) e = hipStreamWaitEvent(r0.s, p->r[r].ev_cols, 0);
     for (uint32_t r = 0; r < N && e == hipSuccess; r++)

@@ -94,6 +94,9 @@ void free_tables(DeviceTables* t);
 hipError_t launch_rs_encode(const RsGeom& g, const DeviceTables& t, hipStream_t s);
 hipError_t launch_rs_encode_bitslice(const RsGeom& g, hipStream_t s);  // GF(2^8), n <= 16
 hipError_t launch_rs_encode_axis(const RsGeom& g, hipStream_t s);       // GF(2^8), 32 <= n <= 128
+// Two launches' worth of GF(2^8) axes (same n, len, axes count and squares, no data copy) in
+// one launch with their tiles interleaved per square (rs_axis.hip, k_rs_axis_gf8_pair).
+hipError_t launch_rs_encode_axis_pair(const RsGeom& g1, const RsGeom& g2, hipStream_t s);
 // Encoding check of listed axes in place in a resident EDS (flags[axis] |= 1 on mismatch),
 // GF(2^8), k = 32, 64, 128.
 hipError_t launch_rs_check_axes(const uint8_t* eds, uint32_t k, const int32_t* idx, int is_col, uint32_t naxes,

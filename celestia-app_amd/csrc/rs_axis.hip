@@ -178,6 +178,43 @@ __global__ __launch_bounds__(256, 3) void k_rs_axis_gf8(RsGeom g, uint32_t nslic
   }
 }
 
+// Two geometries in one launch, tiles interleaved (square z: row tile x, column tile x,
+// row tile x + 1, ...): the extension's Q0 rows -> Q1 beside its Q0 columns -> Q2. Both read
+// Q0, so with the pairs adjacent in the dispatch order the second read of each Q0 line
+// comes from the L2 or the Infinity Cache while the first is recent (default-policy loads
+// allocate there), and the square's Q0 crosses HBM once. The Q1 columns -> Q3 follow in a
+// second launch (they need every Q1 row). HBM bytes per square: Q0 once, Q1 | Q2 written,
+// Q1 read back, Q3 written = 1.25x the algorithmic 2048 k^2 (the rows-then-all-columns
+// order re-reads Q0 and Q1: 1.5x).
+template <int LOGK>
+__global__ __launch_bounds__(256, 3) void k_rs_axis_gf8_pair(RsGeom g1, RsGeom g2, uint32_t nslice) {
+  constexpr int K = 1 << LOGK;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t tile = __builtin_amdgcn_readfirstlane(xcd_block(blockIdx.x, gridDim.x) * 4u + (threadIdx.x >> 6));
+  const uint32_t per_sq = 2u * g1.axes * nslice;
+  if (tile >= per_sq * g1.nsq) return;
+  const uint32_t z = tile / per_sq, r = tile % per_sq, second = r & 1u, rr = r >> 1;
+  const uint32_t y = rr % nslice, x = rr / nslice;
+  const RsGeom& g = second ? g2 : g1;
+  const uint32_t col = y * 256u + lane * 4u;
+  const bool active = col < g.len;
+  const uint32_t lo = active ? lane * 4u : 0u;
+  uint32_t w[K];
+  {
+    const auto rin = rsrc(g.in + (uint64_t)z * g.in_sq + (uint64_t)x * g.in_axis + (uint64_t)y * 256u);
+    const uint32_t in_shard = (uint32_t)g.in_shard;
+#pragma unroll
+    for (int i = 0; i < K; i++) w[i] = __builtin_amdgcn_raw_buffer_load_b32(rin, lo, (uint32_t)i * in_shard, 0);
+  }
+  transform_hyb<K>(w);
+  if (active) {
+    const auto rout = rsrc(g.out + (uint64_t)z * g.out_sq + (uint64_t)x * g.out_axis + (uint64_t)y * 256u);
+    const uint32_t out_shard = (uint32_t)g.out_shard;
+#pragma unroll
+    for (int i = 0; i < K; i++) __builtin_amdgcn_raw_buffer_store_b32(w[i], rout, lo, (uint32_t)i * out_shard, 2);
+  }
+}
+
 template <int LOGK>
 hipError_t launch(const RsGeom& g, hipStream_t s) {
   const uint32_t nslice = (g.len + 255) / 256;
@@ -185,6 +222,16 @@ hipError_t launch(const RsGeom& g, hipStream_t s) {
   if (ntiles == 0) return hipSuccess;
   if (ntiles > 0xFFFFFFF0ull) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_rs_axis_gf8<LOGK>, dim3((unsigned)((ntiles + 3) / 4)), dim3(256), 0, s, g, nslice);
+  return hipGetLastError();
+}
+
+template <int LOGK>
+hipError_t launch_pair(const RsGeom& g1, const RsGeom& g2, hipStream_t s) {
+  const uint32_t nslice = (g1.len + 255) / 256;
+  const uint64_t ntiles = 2ull * g1.axes * nslice * g1.nsq;
+  if (ntiles == 0) return hipSuccess;
+  if (ntiles > 0xFFFFFFF0ull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_rs_axis_gf8_pair<LOGK>, dim3((unsigned)((ntiles + 3) / 4)), dim3(256), 0, s, g1, g2, nslice);
   return hipGetLastError();
 }
 
@@ -232,6 +279,18 @@ hipError_t launch_rs_encode_axis(const RsGeom& g, hipStream_t s) {
     case 32: return ax::launch<5>(g, s);
     case 64: return ax::launch<6>(g, s);
     case 128: return ax::launch<7>(g, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_rs_encode_axis_pair(const RsGeom& g1, const RsGeom& g2, hipStream_t s) {
+  if (!geom_ok(g1) || !geom_ok(g2) || g1.len == 0 || g1.dcopy || g2.dcopy || g1.n != g2.n || g1.len != g2.len ||
+      g1.axes != g2.axes || g1.nsq != g2.nsq)
+    return hipErrorInvalidValue;
+  switch (g1.n) {
+    case 32: return ax::launch_pair<5>(g1, g2, s);
+    case 64: return ax::launch_pair<6>(g1, g2, s);
+    case 128: return ax::launch_pair<7>(g1, g2, s);
     default: return hipErrorInvalidValue;
   }
 }

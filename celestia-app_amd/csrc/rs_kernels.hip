@@ -256,6 +256,21 @@ hipError_t launch_extend(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t 
                          hipStream_t s) {
   if (nsq == 0) return hipSuccess;
   hipError_t e;
+  if (!ods && k >= 32 && k <= kMaxGf8Width) {
+    // GF(2^8) in place: Q0 rows -> Q1 beside Q0 columns -> Q2 (one launch, each Q0 line read
+    // from HBM once), then Q1 columns -> Q3 (rs_axis.hip, k_rs_axis_gf8_pair)
+    const uint64_t half = (uint64_t)k * kShare;
+    RsGeom c0 = col_geom(eds, k, nsq), c1 = c0;
+    c0.axes = c1.axes = k;
+    c1.in += half;
+    c1.out += half;
+    {
+      const Range r("rs.rows+q0cols");
+      if ((e = launch_rs_encode_axis_pair(row_geom(nullptr, eds, k, nsq), c0, s)) != hipSuccess) return e;
+    }
+    const Range r("rs.q1cols");
+    return launch_rs_encode(c1, t, s);
+  }
   // Q0 rows -> Q1 (reading the ODS and writing Q0 into the EDS on the way when ods != nullptr)
   {
     const Range r("rs.rows");

@@ -207,13 +207,16 @@ cel_status cel_extend_sharded(cel_ctx* const* ctxs, uint32_t ngpu, const uint8_t
  *            the DAH (rank 0); returns the square's status (CEL_EORDER) or a device error.
  * flags: CEL_FLAG_ORDER_CHECK, CEL_FLAG_PARITY_ONLY (wait's eds_out), CEL_FLAG_SHARD_EXCHANGE. */
 typedef struct cel_shard_plan cel_shard_plan;
-#define CEL_FLAG_SHARD_EXCHANGE 0x8u /* ngpu = 1: a separate send buffer and the all-to-all run through
-                                        the communicator (self send / receive) instead of the row pass
-                                        writing the slab in place (tests the N > 1 exchange on one GPU) */
+#define CEL_FLAG_SHARD_EXCHANGE 0x8u /* ngpu = 1: a one-rank RCCL communicator, a separate send buffer,
+                                        the all-to-all through it (self send / receive) and the record
+                                        all-gather too, instead of the row pass writing the slab in
+                                        place and no collective (tests the N > 1 exchange on one GPU) */
 cel_status cel_shard_plan_create(cel_ctx* const* ctxs, uint32_t ngpu, uint32_t k, uint32_t flags,
                                  cel_shard_plan** out);
 void cel_shard_plan_destroy(cel_shard_plan* plan);
-const char* cel_shard_plan_transport(const cel_shard_plan* plan); /* "rccl" or "copy" */
+const char* cel_shard_plan_transport(const cel_shard_plan* plan); /* "rccl", "copy" (ctxs repeat a
+                                                                      device) or "local" (one rank,
+                                                                      no collective) */
 const char* cel_shard_plan_last_error(const cel_shard_plan* plan);
 cel_status cel_shard_plan_upload(cel_shard_plan* plan, const uint8_t* ods);
 cel_status cel_shard_plan_run(cel_shard_plan* plan);

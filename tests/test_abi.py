@@ -64,3 +64,28 @@ def test_gfx950_code_object():
     """The library carries a gfx950 code object in its HIP fat binary."""
     data = open(LIB, "rb").read()
     assert b"hipv4-amdgcn-amd-amdhsa--gfx950" in data
+
+
+def test_multi_gpu_entry_points_validate_without_a_device():
+    """The multi-GPU and probe entry points reject missing contexts and outputs before any
+    device or RCCL call (no GPU here): CEL_EINVAL, and a NULL plan handle back."""
+    import ctypes
+    import celestia_eds._lib as L
+    lib = L.load()
+    h = ctypes.c_void_p(123)
+    assert lib.cel_shard_plan_create(None, 1, 256, 0, ctypes.byref(h)) == L.EINVAL
+    assert h.value is None
+    assert lib.cel_shard_plan_create(None, 1, 256, 0, None) == L.EINVAL
+    null_ctxs = (ctypes.c_void_p * 2)(None, None)
+    assert lib.cel_shard_plan_create(null_ctxs, 2, 256, 0, ctypes.byref(h)) == L.EINVAL
+    assert lib.cel_extend_sharded(None, 1, None, 256, 512, None, None, None, None, 0) == L.EINVAL
+    assert lib.cel_extend_batch_multi(None, 2, None, 1, 64, 512, None, None, None, None, None, 0) == L.EINVAL
+    assert lib.cel_extend_batch_multi(null_ctxs, 2, None, 1, 64, 512, None, None, None, None, None, 0) == L.EINVAL
+    assert lib.cel_shard_plan_run(None) == L.EINVAL
+    assert lib.cel_shard_plan_upload(None, None) == L.EINVAL
+    assert lib.cel_shard_plan_wait(None, None, None, None, None) == L.EINVAL
+    assert lib.cel_shard_plan_transport(None) == b""
+    lib.cel_shard_plan_destroy(None)
+    d = ctypes.c_double()
+    assert lib.cel_probe_sha256(None, ctypes.byref(d), None) == L.EINVAL
+    assert lib.cel_probe_hbm_copy(None, 1 << 20, ctypes.byref(d)) == L.EINVAL

@@ -2,9 +2,10 @@
 "multi-GPU" section), through the C ABI:
 
 - cel_extend_sharded / cel_shard_plan_* (config 3): one square row-sharded over the ctxs'
-  devices, collectives issued by the library. On the box's one GPU: a real one-rank RCCL
-  communicator (transport "rccl"; with CEL_FLAG_SHARD_EXCHANGE the all-to-all goes through
-  ncclSend / ncclRecv to self), and N = 2..8 ranks as N ctxs on the same device (transport
+  devices, collectives issued by the library. On the box's one GPU: one rank with no
+  collective (transport "local"), one rank on a real RCCL communicator (CEL_FLAG_SHARD_EXCHANGE:
+  transport "rccl", the all-to-all through ncclSend / ncclRecv to self and the records through
+  ncclAllGather), and N = 2..8 ranks as N ctxs on the same device (transport
   "copy": RCCL refuses two ranks on one device, the plan moves the same blocks with device
   copies in the same schedule). Every EDS byte, root and DAH against the whole-square oracle.
 - cel_extend_batch_multi (config 4): squares split over two ctxs on device 0, one host
@@ -49,21 +50,23 @@ def ctxs():
 
 
 @pytest.mark.parametrize("k", [256, 512])
-def test_extend_sharded_one_rank_rccl(ctxs, oracle, k):
-    """cel_extend_sharded at ngpu = 1: the plan's communicator is a real RCCL one (the record
-    all-gather runs through it), bit-exact against the oracle."""
+def test_extend_sharded_one_rank(ctxs, oracle, k):
+    """cel_extend_sharded at ngpu = 1: no collective is needed (transport "local": the row
+    pass writes the slab in place, the finish reads the rank's own records), bit-exact
+    against the oracle."""
     from celestia_eds.multi import ShardPlan, extend_sharded
     got = extend_sharded(ctxs[:1], random_ods(k, 900 + k))
     assert_square(got, expected(oracle, k, 900 + k))
     plan = ShardPlan(ctxs[:1], k)
-    assert plan.transport == "rccl"
+    assert plan.transport == "local"
     plan.close()
 
 
 @pytest.mark.parametrize("k", [256, 512])
 def test_shard_plan_rccl_exchange(ctxs, oracle, k):
-    """One rank with CEL_FLAG_SHARD_EXCHANGE: the all-to-all is grouped ncclSend / ncclRecv
-    (to itself) on the real communicator, then two more squares through the same plan."""
+    """One rank with CEL_FLAG_SHARD_EXCHANGE, on a real one-rank RCCL communicator: the
+    all-to-all is grouped ncclSend / ncclRecv (to itself) and the records go through
+    ncclAllGather; two squares through the same plan."""
     from celestia_eds import _lib
     from celestia_eds.multi import ShardPlan
     plan = ShardPlan(ctxs[:1], k, _lib.FLAG_ORDER_CHECK | _lib.FLAG_SHARD_EXCHANGE)

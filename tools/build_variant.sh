@@ -19,7 +19,8 @@ if [ "$patch" != "-" ]; then
   (cd $bd/src && patch -p2 --quiet < "$patch")
 fi
 HIPCC=/opt/rocm/bin/hipcc
-srcs="api.cpp api_repair.cpp api_shard.cpp api_trees.cpp square.cpp proof.cpp inclusion.cpp inclusion_paths.cpp rs_kernels.hip rs_bitslice.hip rs_axis.hip rs_decode_axis.hip rs_decode_gf16.hip rs_gf16x.hip nmt_kernels.hip repair_kernels.hip"
+# the library's sources, as the Makefile lists them
+srcs=$(sed -n 's/^SRC := //p' celestia-app_amd/Makefile | sed 's#csrc/##g')
 objs=""
 for f in $srcs; do
   extra=""
@@ -29,6 +30,6 @@ for f in $srcs; do
   objs="$objs $bd/$f.o"
 done
 wait
-$HIPCC --offload-arch=gfx950 -shared -o variants/lib$name.so $objs -L/opt/rocm/lib -lrocprofiler-sdk-roctx \
+$HIPCC --offload-arch=gfx950 -shared -o variants/lib$name.so $objs -L/opt/rocm/lib -lrocprofiler-sdk-roctx -ldl \
   -Wl,-rpath,/opt/rocm/lib
 echo variants/lib$name.so

@@ -1,5 +1,6 @@
 #!/bin/bash
-# Latency-path A/B (variants/lib<v>.so: CEL_DAH_UNROLL / CEL_LEVEL_UNROLL): rank-0 chain of
+# Latency-path A/B of library variants (variants/lib<v>.so, built by build_variant.sh from a
+# tools/variants/*.patch; the shipped sources have no A/B macros): rank-0 chain of
 # a row-sharded k=512 square (N = 1, 8), one k=128 header through the host entry point,
 # k=64 B=128 batch steps, the k=128 repair.
 set -o pipefail
