@@ -148,9 +148,11 @@ def run_distcheck(a):
     A step is a fixed CPU hash of a rank-local buffer (a stand-in for the batch step)."""
     import hashlib
     import torch.distributed as dist
+    global IDLE_GROUP
     world, rank, _ = _dist_env()
     if world > 1:
         dist.init_process_group("gloo")
+        IDLE_GROUP = dist.new_group(backend="gloo")
     buf = np.random.default_rng(rank).integers(0, 256, 1 << 20, dtype=np.uint8).tobytes()
 
     def step():
@@ -192,6 +194,19 @@ def run_distcheck(a):
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             t_a2a = float(t.item())
         riders["rowshard512"] = _rowshard_fields(k, world, elapsed, a.steps, t_a2a)
+
+        # the library riders' assembly: rank 0 alone runs them (a CPU stand-in here) while
+        # the other ranks wait on the gloo idle group
+        def stand_in(name):
+            def fn():
+                t1 = time.perf_counter()
+                for _ in range(a.steps):
+                    step()
+                return {"driver": "library (CPU stand-in)", "devices": list(range(world)),
+                        "value": a.steps / (time.perf_counter() - t1), "unit": "steps/s", "name": name}
+            return fn
+        _library_riders(riders, a, world, rank, dist if world > 1 else None,
+                        {"rowshard512_lib": stand_in("rowshard512_lib"), "k64_lib": stand_in("k64_lib")})
     if rank == 0:
         print(json.dumps({"metric": "distcheck steps/sec", "value": world * a.steps / elapsed, "unit": "steps/s",
                           "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
@@ -858,14 +873,21 @@ def measure_k64_lib(world, steps, warmup, inflight):
             "ms_per_step": el / steps * 1e3, "steps": steps, "squares_per_step_per_gpu": B, "scaling": "strong"}
 
 
-def _library_riders(result, a, world, rank, dist):
+def _library_riders(result, a, world, rank, dist, fns=None):
     """Rank 0 alone drives every GPU of the job through the library (one process, as a Go
     node would): configs 3 and 4. The other ranks wait on a gloo barrier, which puts no work
-    on their GPUs, so rank 0's kernels and RCCL have the devices to themselves."""
-    if rank == 0:
-        _rider(result, "rowshard512_lib", lambda: measure_rowshard_lib(512, world, a.rider_steps, 2, a.depth))
+    on their GPUs, so rank 0's kernels and RCCL have the devices to themselves. fns: the
+    riders by name (default: the GPU measurements; distcheck passes CPU stand-ins)."""
+    if fns is None:
+        fns = {"rowshard512_lib": lambda: measure_rowshard_lib(512, world, a.rider_steps, 2, a.depth)}
         if world > 1:
-            _rider(result, "k64_lib", lambda: measure_k64_lib(world, a.rider_steps, 2, a.inflight))
+            fns["k64_lib"] = lambda: measure_k64_lib(world, a.rider_steps, 2, a.inflight)
+    if rank == 0:
+        for name, fn in fns.items():
+            if torch.cuda.is_available():
+                _rider(result, name, fn)
+            else:
+                result[name] = fn()
     if dist is not None:
         dist.barrier(group=IDLE_GROUP)
 

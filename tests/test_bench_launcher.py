@@ -49,3 +49,7 @@ def test_riders_in_multi_rank_line():
     assert rs["n_gpus"] == 4 and rs["scaling"] == "strong"
     assert rs["a2a_bytes_per_peer"] == 2 * 64 * 64 * 512 // 16
     assert rs["a2a_us"] > 0 and rs["a2a_survey_estimate_us"] > 0
+    # the library riders: rank 0 alone drives every device (here a CPU stand-in) while the
+    # other ranks wait on the gloo idle group; both reach the line with all N devices
+    for name in ("rowshard512_lib", "k64_lib"):
+        assert r[name]["devices"] == [0, 1, 2, 3] and r[name]["value"] > 0
