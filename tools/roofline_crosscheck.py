@@ -40,27 +40,33 @@ def main():
         if ln.startswith("{"):
             line = json.loads(ln)
     nslice = 2  # 512-byte shares in 256-byte slices
-    rows_grid = k * nslice * B // 4 * 256  # k_rs_axis_gf8: 4 tiles (waves) per 256-thread workgroup
-    rs_name = "k_rs_axis_gf8"
-    cand = [r for r in rows if rs_name in r["Kernel_Name"] and int(r["Grid_Size_X"]) == rows_grid]
-    if not cand:
-        sys.exit(f"no {rs_name} launch with grid {rows_grid} in {tdir}")
-    rs_kernel = cand[0]["Kernel_Name"]
-    # the chunk streams' column launches have the full-batch rows grid too: the launch stream
-    # is the one that runs the full-batch column launch (grid 2x)
-    colc = [r for r in rows if r["Kernel_Name"] == rs_kernel and int(r["Grid_Size_X"]) == 2 * rows_grid]
-    stream = collections.Counter((r["Stream_Id"], r["Queue_Id"]) for r in colc).most_common(1)[0][0]
-    cand = [r for r in cand if (r["Stream_Id"], r["Queue_Id"]) == stream]
-    # the k-run's window: from its first full-batch rows launch to the first launch of
+    R = k * nslice * B // 4 * 256  # k axes of B squares: 4 tiles (waves) per 256-thread workgroup
+    # the RS launch pair, by schedule (round 5: rows beside Q0 columns, then Q1 columns)
+    pair_k = [r for r in rows if "k_rs_axis_gf8_pair" in r["Kernel_Name"] and int(r["Grid_Size_X"]) == 2 * R]
+    if pair_k:
+        first_name = pair_k[0]["Kernel_Name"]
+        second_name = next(r["Kernel_Name"] for r in rows if "k_rs_axis_gf8<" in r["Kernel_Name"]
+                           and int(r["Grid_Size_X"]) == R)
+        launches = [(first_name, 2 * R, "rows + Q0 cols"), (second_name, R, "Q1 cols")]
+    else:
+        name = next(r["Kernel_Name"] for r in rows if "k_rs_axis_gf8" in r["Kernel_Name"] and int(r["Grid_Size_X"]) == R)
+        launches = [(name, R, "rows"), (name, 2 * R, "cols")]
+    rs_names = {n for n, _, _ in launches}
+    # the phase timing's stream: the one running most full-batch launches of the 2R-grid kernel
+    big = [ln for ln in launches if ln[1] == 2 * R][0]
+    bigc = [r for r in rows if r["Kernel_Name"] == big[0] and int(r["Grid_Size_X"]) == big[1]]
+    stream = collections.Counter((r["Stream_Id"], r["Queue_Id"]) for r in bigc).most_common(1)[0][0]
+    cand = [r for r in bigc if (r["Stream_Id"], r["Queue_Id"]) == stream]
+    # the k-run's window: from its first full-batch RS launch to the first launch of
     # another RS kernel (the next shape's run: the k=512 line or a rider) after it
     t0 = min(int(r["Start_Timestamp"]) for r in cand)
     later = [int(r["Start_Timestamp"]) for r in rows if int(r["Start_Timestamp"]) > t0
-             and ("k_rs" in r["Kernel_Name"] and r["Kernel_Name"] != rs_kernel)]
+             and ("k_rs" in r["Kernel_Name"] and r["Kernel_Name"] not in rs_names)]
     t1 = min(later) if later else float("inf")
     # --inflight > 1: the timed steps run full-batch launches on every batch's stream, two
     # batches at once; the phase timing (one batch alone) starts after the last of the
     # other batches' launches
-    others = {(r["Stream_Id"], r["Queue_Id"]) for r in colc} - {stream}
+    others = {(r["Stream_Id"], r["Queue_Id"]) for r in bigc} - {stream}
     ends = [int(r["End_Timestamp"]) for r in rows if (r["Stream_Id"], r["Queue_Id"]) in others
             and t0 <= int(r["Start_Timestamp"]) < t1]
     if ends:
@@ -73,20 +79,19 @@ def main():
     P = out.append
     P(f"# roofline cross-check: rocprofv3 --kernel-trace of `python3 bench.py` vs its JSON line")
     P(f"# trace: {tdir}; line: {bjson}; k={k}, B={B}; launch stream {stream[0]} (queue {stream[1]}),")
-    P(f"# the stream of the phase timing's full-batch RS launches (rows grid {rows_grid}), from the first of them")
+    P(f"# the stream of the phase timing's full-batch RS launches, from the first of them")
     P(f"# (with batches in flight: from the other batches' last launch) to the next")
     P(f"# shape's first RS launch ({(t1 - t0) / 1e6 if t1 != float('inf') else 0:.1f} ms); medians over the calls")
     P(f"{'kernel':70s} {'grid':>10s} {'calls':>5s} {'median_us':>10s}")
     for (n, g), v in sorted(d.items(), key=lambda x: -statistics.median(x[1])):
         P(f"{n[:70]:70s} {g:10d} {len(v):5d} {statistics.median(v):10.1f}")
-    rs_rows = statistics.median(d[(rs_kernel, rows_grid)])
-    rs_cols = statistics.median(d[(rs_kernel, 2 * rows_grid)])
-    pair = rs_rows + rs_cols
+    parts = [(what, statistics.median(d[(n, g)])) for n, g, what in launches]
+    pair = sum(t for _, t in parts)
     alg = 2048 * k * k * B
     frac = alg / (pair * 1e-6) / 8e12
     P("")
-    P(f"RS launch pair (rows {rs_rows:.1f} + cols {rs_cols:.1f}) = {pair:.1f} us; algorithmic 2048 k^2 B = "
-      f"{alg / 1e9:.3f} GB -> {alg / pair / 1e3:.0f} GB/s = frac {frac:.4f} of 8 TB/s")
+    P(f"RS launch pair (" + " + ".join(f"{w} {t:.1f}" for w, t in parts) + f") = {pair:.1f} us; algorithmic "
+      f"2048 k^2 B = {alg / 1e9:.3f} GB -> {alg / pair / 1e3:.0f} GB/s = frac {frac:.4f} of 8 TB/s")
     nmt_keys = [(n, g) for (n, g) in d if any(s in n for s in ("k_leaf", "k_level", "k_merkle", "k_dah"))]
     # commit_only runs every NMT kernel once per call at the full-batch grids on this stream
     nmt = sum(statistics.median(d[key]) for key in nmt_keys)
