@@ -57,7 +57,7 @@ SHA_MEASURED_PEAK = 29.4e9
 SHA_GUIDE_CEILING = 1024 * 2.4e9 * 64 / (2 * 1414)
 # Measured HBM traffic of the RS extension (rocprofv3 FETCH_SIZE/WRITE_SIZE passes).
 # (input layout -> profile): ODS in Q0 of the EDS (in place) / separate ODS buffer.
-TRAFFIC_PROFILE = {"eds": "r4_rs_traffic_inplace.json", "ods": "r1_rs_traffic.json"}
+TRAFFIC_PROFILE = {"eds": "r5_rs_traffic_inplace.json", "ods": "r1_rs_traffic.json"}
 
 
 def _rs_traffic(k, batch, layout):
