@@ -193,8 +193,13 @@ __global__ __launch_bounds__(256, 3) void k_rs_axis_gf8_pair(RsGeom g1, RsGeom g
   const uint32_t tile = __builtin_amdgcn_readfirstlane(xcd_block(blockIdx.x, gridDim.x) * 4u + (threadIdx.x >> 6));
   const uint32_t per_sq = 2u * g1.axes * nslice;
   if (tile >= per_sq * g1.nsq) return;
+  // k = 128: slice-major inside a square, so the 2k tiles of one 256-byte slice run together
+  // and the Q0 bytes they share (k^2 x 256 B = 4 MiB, one XCD's L2) stay resident between
+  // the row tile's read and the column tile's: Q0 is fetched once (PMC: 1.00x of Q0 against
+  // 1.47x with the slices interleaved, profiles/r5_rs_slice_ab.txt). At k <= 64 both slices
+  // of a square fit together and the interleaved order measured 2 % faster.
   const uint32_t z = tile / per_sq, r = tile % per_sq, second = r & 1u, rr = r >> 1;
-  const uint32_t y = rr % nslice, x = rr / nslice;
+  const uint32_t y = LOGK >= 7 ? rr / g1.axes : rr % nslice, x = LOGK >= 7 ? rr % g1.axes : rr / nslice;
   const RsGeom& g = second ? g2 : g1;
   const uint32_t col = y * 256u + lane * 4u;
   const bool active = col < g.len;
