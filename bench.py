@@ -90,7 +90,7 @@ def parse():
                     help="eds: the upload places each ODS in Q0 of its EDS buffer and the extension "
                          "reads it in place; ods: separate contiguous ODS buffer, the row pass copies Q0")
     ap.add_argument("--phase-reps", type=int, default=10)
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=3,
                     help="batches in flight: steps go round-robin over this many batches, each with its own "
                          "buffers and stream (independent blocks back to back, CEL_FLAG_CALLER_STREAM); "
                          "1 = one batch, each step split in two chunks on the library's internal streams")
@@ -962,7 +962,7 @@ def _measure_batch(ctx, local, rank, k, B, steps, warmup, n_distinct, layout, ph
     return {"sb": sb, "distinct": distinct, "elapsed": elapsed, "t_ext": t_ext, "t_com": t_com}
 
 
-def measure_host_io(ctx, k, n=16, reps=3):
+def measure_host_io(ctx, k, n=16, reps=5):
     """cel_extend_batch over page-locked host buffers (cel_host_alloc): n ODSs in, then
     (a) the EDS + roots + DAH out (what rsmt2d.ImportExtendedDataSquare needs) and
     (b) the parity cells only (CEL_FLAG_PARITY_ONLY: the caller holds Q0 already) and
@@ -994,7 +994,8 @@ def measure_host_io(ctx, k, n=16, reps=3):
             def once():
                 ctx.check(ctx.lib.cel_extend_batch(ctx.handle, P(ods), n, k, 512, P(e) if e is not None else None,
                                                    P(rr), P(cr), P(dah), P(st), _lib.FLAG_ORDER_CHECK | fl))
-            once()
+            for _ in range(3):  # warm: the first calls after the riders ran 30-40 % slower
+                once()
             t0 = time.perf_counter()
             for _ in range(reps):
                 once()

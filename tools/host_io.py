@@ -17,6 +17,7 @@ ap.add_argument("--batch", type=int, default=16)
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--no-eds", action="store_true", help="roots + DAH only (no EDS copy back)")
 ap.add_argument("--pinned", action="store_true", help="ODS / EDS buffers from cel_host_alloc (page-locked)")
+ap.add_argument("--parity-only", action="store_true", help="CEL_FLAG_PARITY_ONLY: Q1..Q3 of the EDS back, not Q0")
 a = ap.parse_args()
 from celestia_eds import _lib  # noqa: E402
 from celestia_eds.testfactory import random_ods  # noqa: E402
@@ -48,7 +49,7 @@ P = lambda x: x.ctypes.data_as(ctypes.c_void_p) if x is not None else None
 
 def once():
     ctx.check(ctx.lib.cel_extend_batch(ctx.handle, P(ods), n, k, 512, P(eds), P(rr), P(cr), P(dah), P(st),
-                                       _lib.FLAG_ORDER_CHECK))
+                                       _lib.FLAG_ORDER_CHECK | (_lib.FLAG_PARITY_ONLY if a.parity_only else 0)))
 
 
 once()
@@ -56,6 +57,7 @@ t0 = time.perf_counter()
 for _ in range(a.reps):
     once()
 dt = (time.perf_counter() - t0) / a.reps
-mode = ("ODS in, roots+DAH out" if a.no_eds else "ODS in, EDS+roots+DAH out") + (", pinned" if a.pinned else ", pageable")
+mode = ("ODS in, roots+DAH out" if a.no_eds else
+        "ODS in, parity quadrants+roots+DAH out" if a.parity_only else "ODS in, EDS+roots+DAH out") + (", pinned" if a.pinned else ", pageable")
 print(f"host-buffer cel_extend_batch k={k} batch={n} ({mode}): {dt * 1e3:.2f} ms per call = "
       f"{n / dt:.0f} squares/s; bytes over PCIe {(ods.nbytes + (0 if eds is None else eds.nbytes)) / dt / 1e9:.1f} GB/s")
