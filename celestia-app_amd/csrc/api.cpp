@@ -309,13 +309,14 @@ static const uint8_t* mapped_host(const uint8_t* p) {
 //     writes Q0 and Q1 (the upload and the row transform are one launch);
 //     pageable ODS: one contiguous copy to the device first, then the row pass;
 //   - the column pass, every leaf, the tree levels and the DAH;
-//   - every result in one copy into page-locked staging (separate copies into pageable
-//     memory cost a staging kernel and a host wait each).
+//   - the DAH launch writes every result (roots, DAH, status) into page-locked staging
+//     itself (round 4: four copies into pageable memory, each a staging kernel and a host
+//     wait; round 5 first: one copy after the DAH launch).
 // The EDS download, if asked for, runs on a download stream after the column pass.
 static cel_status extend_one(cel_ctx* ctx, const uint8_t* ods, uint32_t k, uint8_t* eds_out, uint8_t* row_roots,
                              uint8_t* col_roots, uint8_t* dah, int32_t* status_out, uint32_t flags) {
   const size_t ods_b = (size_t)k * k * kShare, eds_b = 4 * ods_b, roots_b = (size_t)2 * k * kNode;
-  const size_t out_b = 2 * roots_b + 32 + 4;
+  const size_t out_b = (2 * roots_b + 32 + 4 + 15) & ~(size_t)15;
   hipError_t e = hipSuccess;
   const uint8_t* src = mapped_host(ods);
   uint8_t* d_eds = static_cast<uint8_t*>(scratch(ctx, S_EDS, eds_b, &e));
@@ -324,6 +325,8 @@ static cel_status extend_one(cel_ctx* ctx, const uint8_t* ods, uint32_t k, uint8
   uint8_t* d_out = static_cast<uint8_t*>(scratch(ctx, S_ROOTS, out_b, &e));
   uint8_t* h_out = static_cast<uint8_t*>(host_stage(ctx, out_b));
   if (!d_eds || (!src && !d_ods) || !d_work || !d_out || !h_out) return fail(ctx, CEL_ENOMEM, "allocation failed");
+  uint8_t* h_dev = const_cast<uint8_t*>(mapped_host(h_out));
+  if (!h_dev) return fail(ctx, CEL_EDEVICE, "page-locked staging is not mapped for the device");
   int32_t* d_st = reinterpret_cast<int32_t*>(d_out + 2 * roots_b + 32);
   hipStream_t s = ctx->stream, d = ctx->dl[0];
   auto enqueue = [&]() -> hipError_t {
@@ -338,9 +341,11 @@ static cel_status extend_one(cel_ctx* ctx, const uint8_t* ods, uint32_t k, uint8
     if (eds_out &&
         ((r = hipEventRecord(ctx->ev_rs[0], s)) != hipSuccess || (r = hipStreamWaitEvent(d, ctx->ev_rs[0], 0))))
       return r;
-    if ((r = launch_commit(d_eds, k, 1, d_out, d_out + roots_b, d_out + 2 * roots_b, d_st, d_work,
-                           (flags & CEL_FLAG_ORDER_CHECK) != 0, s)) != hipSuccess ||
-        (r = hipMemcpyAsync(h_out, d_out, out_b, hipMemcpyDeviceToHost, s)) != hipSuccess)
+    // the DAH launch writes every result into the page-locked staging itself
+    if ((r = launch_commit_leaves(d_eds, k, 1, d_work, (flags & CEL_FLAG_ORDER_CHECK) != 0, 0, 2 * k, true, s)) !=
+            hipSuccess ||
+        (r = launch_commit_trees(k, 1, d_out, d_out + roots_b, d_out + 2 * roots_b, d_st, d_work, s, h_dev,
+                                 (uint32_t)out_b)) != hipSuccess)
       return r;
     if (eds_out) {
       // after every kernel is enqueued: a copy into pageable memory blocks the calling thread

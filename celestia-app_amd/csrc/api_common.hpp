@@ -44,7 +44,8 @@ inline void* host_stage(cel_ctx* ctx, size_t bytes) {
   if (ctx->hstage) (void)hipHostFree(ctx->hstage);
   ctx->hstage = nullptr;
   ctx->hstage_size = 0;
-  if (hipHostMalloc(&ctx->hstage, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+  // coherent: kernels may store results into it directly (the one-square DAH launch)
+  if (hipHostMalloc(&ctx->hstage, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return nullptr;
   ctx->hstage_size = bytes;
   return ctx->hstage;
 }

@@ -123,8 +123,12 @@ hipError_t launch_commit(const uint8_t* eds, uint32_t k, uint32_t nsq, uint8_t* 
 // commit in stream order), then, after every leaf, the tree levels, roots and DAH.
 hipError_t launch_commit_leaves(const uint8_t* eds, uint32_t k, uint32_t nsq, void* work, bool order_check,
                                 uint32_t row0, uint32_t row1, bool init_bad, hipStream_t s);
+// host_out (nsq == 1, optional): page-locked host memory that receives out_bytes (a multiple of
+// 16) starting at row_roots from the DAH launch itself; row_roots, col_roots, dah and status
+// must then be one contiguous block in that order.
 hipError_t launch_commit_trees(uint32_t k, uint32_t nsq, uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah,
-                               int32_t* status, void* work, hipStream_t s);
+                               int32_t* status, void* work, hipStream_t s, uint8_t* host_out = nullptr,
+                               uint32_t out_bytes = 0);
 // One erasured axis root (cells contiguous) or plain NMT root over leaves.
 hipError_t launch_axis_root(const uint8_t* cells, uint32_t k, uint32_t axis, uint8_t* root,
                             void* work, hipStream_t s);

@@ -391,10 +391,15 @@ __device__ __forceinline__ void sha_empty(uint32_t (&st)[8]) {
 
 // One workgroup per item list: items[g][n] 96-byte records -> 32-byte root (BE words in
 // out[g*8..]). Also packs the first n items into 90-byte outputs (row/col roots) if given.
+// out_src / host_out (one square, optional): after the DAH, the workgroup copies out_bytes
+// (a multiple of 16) from out_src (roots | dah | status, written before the copy) to host_out,
+// page-locked host memory, with 16-byte stores: the results cross PCIe inside this launch
+// instead of in a separate copy after it.
 __global__ __launch_bounds__(1024) void k_merkle(const uint32_t* __restrict__ items, const uint32_t* __restrict__ leafd,
                                                 uint32_t n, uint8_t* __restrict__ dah, uint8_t* __restrict__ row_out,
                                                 uint8_t* __restrict__ col_out, const int32_t* __restrict__ bad_axis,
-                                                int32_t* __restrict__ status) {
+                                                int32_t* __restrict__ status, const uint8_t* __restrict__ out_src = nullptr,
+                                                uint8_t* __restrict__ host_out = nullptr, uint32_t out_bytes = 0) {
   extern __shared__ __attribute__((aligned(16))) uint32_t hs[];  // n * 8 words
   const uint32_t g = blockIdx.x;
   const uint32_t* it = items + (uint64_t)g * n * kNodeWords;
@@ -452,6 +457,13 @@ __global__ __launch_bounds__(1024) void k_merkle(const uint32_t* __restrict__ it
       dah[g * 32 + 4 * j + 3] = (uint8_t)st[j];
     }
     if (status) status[g] = (bad_axis && bad_axis[g] != INT_MAX) ? CEL_EORDER : CEL_OK;
+  }
+  if (host_out) {
+    __threadfence();  // thread 0's dah / status stores before the workgroup reads them back
+    __syncthreads();
+    const uint4* src = reinterpret_cast<const uint4*>(out_src);
+    uint4* dst = reinterpret_cast<uint4*>(host_out);
+    for (uint32_t i = threadIdx.x; i < out_bytes / 16; i += blockDim.x) dst[i] = src[i];
   }
 }
 
@@ -547,7 +559,7 @@ hipError_t launch_commit_leaves(const uint8_t* eds, uint32_t k, uint32_t nsq, vo
 }
 
 hipError_t launch_commit_trees(uint32_t k, uint32_t nsq, uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah,
-                               int32_t* status, void* work, hipStream_t s) {
+                               int32_t* status, void* work, hipStream_t s, uint8_t* host_out, uint32_t out_bytes) {
   const uint32_t W = 2 * k;
   const CommitWork w = commit_work(work, k, nsq);
   // One launch per tree level, all 4k trees of all squares at once: every lane hashes
@@ -578,7 +590,7 @@ hipError_t launch_commit_trees(uint32_t k, uint32_t nsq, uint8_t* row_roots, uin
   const Range r("dah");
   if (dah)
     hipLaunchKernelGGL(k_merkle, dim3(nsq), dim3(merkle_block(trees)), lds, s, w.roots, w.leafd, trees, dah, nullptr,
-                       nullptr, w.bad, status);
+                       nullptr, w.bad, status, host_out ? row_roots : nullptr, host_out, out_bytes);
   return hipGetLastError();
 }
 
