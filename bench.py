@@ -107,7 +107,9 @@ def parse():
                     help="multi-rank rehearsal on a one-GPU box: every rank on cuda:0, gloo instead of RCCL "
                          "(collectives staged through host memory); exercises the N-rank code path, its "
                          "numbers are not multi-GPU measurements")
-    ap.add_argument("--mode", default="batch", choices=["batch", "sharded", "repair", "distcheck"],
+    ap.add_argument("--lib-devices", type=int, default=1,
+                    help="--mode libriders: devices the one process drives (rank 0's child in an N-GPU run)")
+    ap.add_argument("--mode", default="batch", choices=["batch", "sharded", "repair", "distcheck", "libriders"],
                     help="batch: independent squares per GPU (configs 2, 4); sharded: one square "
                          "row-sharded over the ranks (config 3); repair: rsmt2d Repair (config 5); "
                          "distcheck: the launcher / rendezvous / timing contract on CPU ranks over gloo "
@@ -873,20 +875,56 @@ def measure_k64_lib(world, steps, warmup, inflight):
             "ms_per_step": el / steps * 1e3, "steps": steps, "squares_per_step_per_gpu": B, "scaling": "strong"}
 
 
+LIB_RIDER_TIMEOUT_S = 300
+
+
+def run_libriders(a):
+    """--mode libriders: the library riders in a process of their own (rank 0's child in the
+    N-GPU line): one process, every device of the job, RCCL inside the library. Prints one
+    JSON object {rider name: fields}."""
+    global REHEARSE
+    REHEARSE = a.rehearse
+    world = a.lib_devices
+    out = {}
+    torch.cuda.set_device(0)
+    _rider(out, "rowshard512_lib", lambda: measure_rowshard_lib(512, world, a.rider_steps, 2, a.depth))
+    if world > 1:
+        _rider(out, "k64_lib", lambda: measure_k64_lib(world, a.rider_steps, 2, a.inflight))
+    print(json.dumps(out), flush=True)
+
+
+def _spawn_libriders(a, world):
+    """The library riders in a child process with a time limit, so a hang there (RCCL
+    communicator setup over N devices, say) cannot take the headline line with it; rank 0's
+    own GPU state is not shared with the child."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--mode", "libriders", "--lib-devices", str(world),
+           "--rider-steps", str(a.rider_steps), "--depth", str(a.depth), "--inflight", str(a.inflight)]
+    if a.rehearse:
+        cmd.append("--rehearse")
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "GROUP_RANK",
+                                                          "LOCAL_WORLD_SIZE", "ROLE_RANK", "ROLE_WORLD_SIZE")}
+    try:
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=LIB_RIDER_TIMEOUT_S, env=env)
+    except subprocess.TimeoutExpired:
+        err = {"error": f"library riders timed out after {LIB_RIDER_TIMEOUT_S} s"}
+        return {"rowshard512_lib": err, "k64_lib": err} if world > 1 else {"rowshard512_lib": err}
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    if p.returncode != 0 or not lines:
+        err = {"error": f"library riders exited {p.returncode}: {p.stderr[-300:]}"}
+        return {"rowshard512_lib": err}
+    return json.loads(lines[-1])
+
+
 def _library_riders(result, a, world, rank, dist, fns=None):
     """Rank 0 alone drives every GPU of the job through the library (one process, as a Go
-    node would): configs 3 and 4. The other ranks wait on a gloo barrier, which puts no work
-    on their GPUs, so rank 0's kernels and RCCL have the devices to themselves. fns: the
-    riders by name (default: the GPU measurements; distcheck passes CPU stand-ins)."""
-    if fns is None:
-        fns = {"rowshard512_lib": lambda: measure_rowshard_lib(512, world, a.rider_steps, 2, a.depth)}
-        if world > 1:
-            fns["k64_lib"] = lambda: measure_k64_lib(world, a.rider_steps, 2, a.inflight)
+    node would): configs 3 and 4, in a child process (_spawn_libriders). The other ranks wait
+    on a gloo barrier, which puts no work on their GPUs, so the child's kernels and RCCL have
+    the devices to themselves. fns: CPU stand-ins by name, run in rank 0 itself (distcheck)."""
     if rank == 0:
-        for name, fn in fns.items():
-            if torch.cuda.is_available():
-                _rider(result, name, fn)
-            else:
+        if fns is None:
+            result.update(_spawn_libriders(a, world))
+        else:
+            for name, fn in fns.items():
                 result[name] = fn()
     if dist is not None:
         dist.barrier(group=IDLE_GROUP)
@@ -1045,6 +1083,8 @@ def main():
         return run_sharded(a)
     if a.mode == "repair":
         return run_repair(a)
+    if a.mode == "libriders":
+        return run_libriders(a)
     local = _rank_device(local)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
