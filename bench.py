@@ -90,7 +90,7 @@ def parse():
                     help="eds: the upload places each ODS in Q0 of its EDS buffer and the extension "
                          "reads it in place; ods: separate contiguous ODS buffer, the row pass copies Q0")
     ap.add_argument("--phase-reps", type=int, default=10)
-    ap.add_argument("--inflight", type=int, default=3,
+    ap.add_argument("--inflight", type=int, default=4,
                     help="batches in flight: steps go round-robin over this many batches, each with its own "
                          "buffers and stream (independent blocks back to back, CEL_FLAG_CALLER_STREAM); "
                          "1 = one batch, each step split in two chunks on the library's internal streams")
