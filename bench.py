@@ -15,6 +15,10 @@ Besides the headline number the JSON line carries:
   roofline_nmt  NMT+DAH phase: SHA-256 compressions (60 k^2 + 4k - 2 per square)
                 per second vs the measured SHA-256 peak of the same compression code with
                 no memory traffic (and, as peak_model, the op-rate model of its mix)
+  probe         same-run ceilings (cel_probe_*): SHA-256 in registers, shader clock, a
+                streaming copy, and the GF(2^8) encode transform with no HBM traffic
+  roofline_step the whole step per square against the VALU time of its two instruction
+                streams (NMT compressions at the probe's SHA-256 rate + the transform alone)
   k512          (default --k 128 run) the same measurement on a short batch of k=512
                 squares (GF(2^16)), since the metric names k=128 and k=512
   cpu_baseline  the C restatement (oracle/, SIMD + OpenMP) on a bounded sample of the
@@ -769,6 +773,31 @@ def measure_probe(ctx):
     return probe(ctx, 4 << 30)
 
 
+def step_ceiling(k, probe, secs_per_square):
+    """The whole step against the VALU time of its two instruction streams, both same-run:
+    the square's NMT compressions at the SHA-256 probe's rate plus its GF(2^8) extension's
+    transform alone (cel_probe_rs_transform). Both halves are VALU-issue bound, so their sum
+    is the step's floor with these kernels; frac = that floor / the measured time per square
+    on one GPU (overlap of the RS's memory time with the other batches' hashing is what
+    lets it reach 1)."""
+    rs_us = probe.get(f"rs_transform_us_k{k}")
+    if rs_us is None:
+        return None
+    nmt_us = (60 * k * k + 4 * k - 2) / (probe["sha256_gcomp_per_s"] * 1e9) * 1e6
+    meas_us = secs_per_square * 1e6
+    return {
+        "bound": "valu",
+        "unit": "us per square per GPU",
+        "nmt_us": nmt_us,
+        "rs_transform_us": rs_us,
+        "peak": nmt_us + rs_us,
+        "achieved": meas_us,
+        "frac": (nmt_us + rs_us) / meas_us,
+        "basis": "(60k^2 + 4k - 2) compressions / cel_probe_sha256 + cel_probe_rs_transform (the encode "
+                 "tile with no HBM traffic, 3k axis encodes); both kernels' time is VALU issue",
+    }
+
+
 def _lib_devices(world):
     """The devices rank 0 drives in one process for the library riders: one per rank (all on
     cuda:0 in a --rehearse run, where the plan's transport is device copies)."""
@@ -1182,6 +1211,9 @@ def main():
         result["roofline_nmt"]["peak_same_run"] = probe["sha256_gcomp_per_s"]
         result["roofline_nmt"]["frac_same_run"] = nmt_rate / 1e9 / probe["sha256_gcomp_per_s"]
         result["shader_mhz"] = probe["shader_mhz"]
+        step = step_ceiling(k, probe, elapsed / (B * a.steps))
+        if step:
+            result["roofline_step"] = step
 
     if a.k == 128 and a.k512_batch > 0:
         # The metric names k=128 and k=512: a short GF(2^16) batch rides along with the
@@ -1219,7 +1251,11 @@ def main():
         def k64():
             m4 = _measure_batch(ctx, local, rank, 64, 1024 // world, a.rider_steps, 2, 4, a.input, 3, barrier,
                                 dist, dev, a.inflight)
-            return _k64_fields(world, m4["elapsed"], a.rider_steps, m4["t_ext"], m4["t_com"], 1024 // world)
+            f = _k64_fields(world, m4["elapsed"], a.rider_steps, m4["t_ext"], m4["t_com"], 1024 // world)
+            step = step_ceiling(64, probe, m4["elapsed"] / (a.rider_steps * (1024 // world))) if probe else None
+            if step:
+                f["step_valu_us"], f["step_valu_frac"] = step["peak"], step["frac"]
+            return f
 
         _rider(result, "k64", k64)
         if world > 1:  # per-rank processes, torch.distributed's RCCL (at N = 1: rowshard512_lib alone)

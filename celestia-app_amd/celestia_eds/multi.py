@@ -119,10 +119,17 @@ def extend_batch_multi(ctxs, ods, want_eds=True, flags=_lib.FLAG_ORDER_CHECK):
     return eds, rr, cr, dah, st
 
 
-def probe(ctx, hbm_bytes=4 << 30):
+def probe(ctx, hbm_bytes=4 << 30, rs_k=(64, 128)):
     """Same-run ceilings on ctx's device: SHA-256 G compressions/s in registers, the
-    sustained shader clock over that launch (MHz) and streaming-copy HBM GB/s."""
+    sustained shader clock over that launch (MHz), streaming-copy HBM GB/s, and the
+    microseconds of VALU one k-square's GF(2^8) extension takes with no HBM traffic
+    (`rs_transform_us_k<k>`, each k in rs_k)."""
     g, mhz, bw = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
     ctx.check(ctx.lib.cel_probe_sha256(ctx.handle, ctypes.byref(g), ctypes.byref(mhz)))
     ctx.check(ctx.lib.cel_probe_hbm_copy(ctx.handle, hbm_bytes, ctypes.byref(bw)))
-    return {"sha256_gcomp_per_s": g.value, "shader_mhz": mhz.value, "hbm_copy_gbps": bw.value}
+    out = {"sha256_gcomp_per_s": g.value, "shader_mhz": mhz.value, "hbm_copy_gbps": bw.value}
+    for k in rs_k:
+        us = ctypes.c_double()
+        ctx.check(ctx.lib.cel_probe_rs_transform(ctx.handle, k, ctypes.byref(us)))
+        out[f"rs_transform_us_k{k}"] = us.value
+    return out

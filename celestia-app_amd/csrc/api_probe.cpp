@@ -106,4 +106,25 @@ cel_status cel_probe_hbm_copy(cel_ctx* ctx, uint64_t bytes, double* gbps) {
   return CEL_OK;
 }
 
+cel_status cel_probe_rs_transform(cel_ctx* ctx, uint32_t k, double* us_per_square) {
+  if (!ctx || !us_per_square || (k != 32 && k != 64 && k != 128)) return CEL_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  DeviceGuard g(ctx->device);
+  // one square's extension = 3 passes x k axes x 2 slices of 256 B; time 2^17 / k squares'
+  // worth (196,608 tiles at k = 128: ~770 waves per CU)
+  const uint32_t per_sq = 3 * k * (kShare / 256), nsq = (1u << 17) / k, ntiles = per_sq * nsq;
+  hipError_t e = hipSuccess;
+  uint8_t* buf = static_cast<uint8_t*>(scratch(ctx, S_AUX, (size_t)2 * k * 256, &e));
+  if (!buf) return fail(ctx, CEL_ENOMEM, "device allocation failed");
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(buf);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(buf + (size_t)k * 256);
+  hipStream_t s = ctx->stream;
+  if ((e = hipMemsetAsync(buf, 0x3C, (size_t)k * 256, s)) != hipSuccess) return hip_fail(ctx, e, "rs probe");
+  double secs = 0;
+  e = best_time([&] { return launch_probe_rs_transform(k, src, dst, ntiles, 0, s); }, 5, s, &secs);
+  if (e != hipSuccess) return hip_fail(ctx, e, "rs probe");
+  *us_per_square = secs / nsq * 1e6;
+  return CEL_OK;
+}
+
 }  // extern "C"

@@ -171,6 +171,10 @@ hipError_t launch_shard_finish(const uint32_t* gathered, uint32_t k, uint32_t nr
 // clk: 2 counters per wave), and a streaming copy of `bytes` (a multiple of 16).
 hipError_t launch_probe_sha(uint32_t* out, unsigned long long* clk, uint32_t blocks, int n, hipStream_t s);
 hipError_t launch_probe_copy(const void* src, void* dst, uint64_t bytes, uint32_t blocks, bool nt, hipStream_t s);
+// GF(2^8) encode transform alone (rs_axis.hip), k = 32/64/128: ntiles tiles reading the same
+// k x 256 B of src; dst (k x 256 B) written only when store != 0.
+hipError_t launch_probe_rs_transform(uint32_t k, const uint32_t* src, uint32_t* dst, uint32_t ntiles, uint32_t store,
+                                     hipStream_t s);
 
 // Repair helpers (repair_kernels.hip, nmt_kernels.hip).
 hipError_t launch_gather_axes(const uint8_t* eds, const uint8_t* mask, uint32_t W, const int32_t* idx, int is_col,

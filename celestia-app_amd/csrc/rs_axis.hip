@@ -220,6 +220,30 @@ __global__ __launch_bounds__(256, 3) void k_rs_axis_gf8_pair(RsGeom g1, RsGeom g
   }
 }
 
+// Same-run probe of the transform alone (cel_probe_rs_transform): the encode tile's
+// instruction stream with its HBM traffic taken away. Every wave loads the same K x 256 B
+// (one 32 KiB region, cache-resident) and stores only when `store` is set (never, in the
+// probe: the runtime flag keeps the transform live), so the launch time is the VALU time
+// of ntiles tiles.
+template <int LOGK>
+__global__ __launch_bounds__(256, 3) void k_probe_rs_transform(const uint32_t* src, uint32_t* dst, uint32_t ntiles,
+                                                               uint32_t store) {
+  constexpr int K = 1 << LOGK;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t tile = __builtin_amdgcn_readfirstlane(xcd_block(blockIdx.x, gridDim.x) * 4u + (threadIdx.x >> 6));
+  if (tile >= ntiles) return;
+  uint32_t w[K];
+  const auto rin = rsrc(src);
+#pragma unroll
+  for (int i = 0; i < K; i++) w[i] = __builtin_amdgcn_raw_buffer_load_b32(rin, lane * 4u, (uint32_t)i * 256u, 0);
+  transform_hyb<K>(w);
+  if (store) {
+    const auto rout = rsrc(dst);
+#pragma unroll
+    for (int i = 0; i < K; i++) __builtin_amdgcn_raw_buffer_store_b32(w[i], rout, lane * 4u, (uint32_t)i * 256u, 0);
+  }
+}
+
 template <int LOGK>
 hipError_t launch(const RsGeom& g, hipStream_t s) {
   const uint32_t nslice = (g.len + 255) / 256;
@@ -298,6 +322,19 @@ hipError_t launch_rs_encode_axis_pair(const RsGeom& g1, const RsGeom& g2, hipStr
     case 128: return ax::launch_pair<7>(g1, g2, s);
     default: return hipErrorInvalidValue;
   }
+}
+
+hipError_t launch_probe_rs_transform(uint32_t k, const uint32_t* src, uint32_t* dst, uint32_t ntiles, uint32_t store,
+                                     hipStream_t s) {
+  if (ntiles == 0) return hipSuccess;
+  const dim3 grid((ntiles + 3) / 4);
+  switch (k) {
+    case 32: hipLaunchKernelGGL(ax::k_probe_rs_transform<5>, grid, dim3(256), 0, s, src, dst, ntiles, store); break;
+    case 64: hipLaunchKernelGGL(ax::k_probe_rs_transform<6>, grid, dim3(256), 0, s, src, dst, ntiles, store); break;
+    case 128: hipLaunchKernelGGL(ax::k_probe_rs_transform<7>, grid, dim3(256), 0, s, src, dst, ntiles, store); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
 }
 
 hipError_t launch_rs_check_axes(const uint8_t* eds, uint32_t k, const int32_t* idx, int is_col, uint32_t naxes,

@@ -89,3 +89,4 @@ def test_multi_gpu_entry_points_validate_without_a_device():
     d = ctypes.c_double()
     assert lib.cel_probe_sha256(None, ctypes.byref(d), None) == L.EINVAL
     assert lib.cel_probe_hbm_copy(None, 1 << 20, ctypes.byref(d)) == L.EINVAL
+    assert lib.cel_probe_rs_transform(None, 128, ctypes.byref(d)) == L.EINVAL
