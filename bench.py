@@ -904,7 +904,7 @@ def measure_k64_lib(world, steps, warmup, inflight):
             "ms_per_step": el / steps * 1e3, "steps": steps, "squares_per_step_per_gpu": B, "scaling": "strong"}
 
 
-LIB_RIDER_TIMEOUT_S = 300
+LIB_RIDER_TIMEOUT_S = 180
 
 
 def run_libriders(a):
