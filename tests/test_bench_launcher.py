@@ -53,3 +53,17 @@ def test_riders_in_multi_rank_line():
     # other ranks wait on the gloo idle group; both reach the line with all N devices
     for name in ("rowshard512_lib", "k64_lib"):
         assert r[name]["devices"] == [0, 1, 2, 3] and r[name]["value"] > 0
+
+
+def test_step_ceiling_fields():
+    """roofline_step: the square's compressions at the probe's SHA-256 rate plus the
+    transform probe, against the measured time per square (bench.step_ceiling)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    probe = {"sha256_gcomp_per_s": 28.0, "rs_transform_us_k128": 7.5}
+    s = bench.step_ceiling(128, probe, 45e-6)
+    nmt = (60 * 128 * 128 + 4 * 128 - 2) / 28e9 * 1e6
+    assert abs(s["nmt_us"] - nmt) < 1e-9 and s["rs_transform_us"] == 7.5
+    assert abs(s["peak"] - (nmt + 7.5)) < 1e-9 and abs(s["achieved"] - 45.0) < 1e-9
+    assert abs(s["frac"] - (nmt + 7.5) / 45.0) < 1e-12 and s["bound"] == "valu"
+    assert bench.step_ceiling(512, probe, 1e-3) is None  # no GF(2^16) transform probe

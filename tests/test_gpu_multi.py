@@ -151,13 +151,13 @@ def test_extend_sharded_rejects(ctxs):
     assert e.value.status == _lib.EINVAL
 
 
-@pytest.mark.parametrize("k,n", [(64, 5), (128, 3), (32, 8)])
-def test_extend_batch_multi_two_ctxs(ctxs, oracle, k, n):
-    """cel_extend_batch_multi over two ctxs on device 0 (one host thread each): every square
-    of an uneven split equals the oracle."""
+@pytest.mark.parametrize("k,n,g", [(64, 5, 2), (128, 3, 2), (32, 8, 2), (32, 13, 4), (64, 3, 8)])
+def test_extend_batch_multi_two_ctxs(ctxs, oracle, k, n, g):
+    """cel_extend_batch_multi over g ctxs on device 0 (one host thread each): every square
+    of an uneven split equals the oracle, including more ctxs than squares (g = 8, n = 3)."""
     from celestia_eds.multi import extend_batch_multi
     ods = np.stack([random_ods(k, 960 + i) for i in range(n)])
-    eds, rr, cr, dah, st = extend_batch_multi(ctxs[:2], ods)
+    eds, rr, cr, dah, st = extend_batch_multi(ctxs[:g], ods)
     assert (st == 0).all()
     for i in range(n):
         w_eds, w_rr, w_cr, w_dah = oracle.extend_and_commit(ods[i])
