@@ -1,7 +1,8 @@
 """The C ABI from plain C (tests/c_abi_client.c), as the cgo stub binds it: the header
 compiles as C99 with gcc and the client links against libcelestia_eds.so. Here (no GPU)
 the client must get CEL_EDEVICE from cel_ctx_create (no CPU fallback); on the MI355X it
-checks the k = 2 DAH known answer, the DAH-only call and the power-of-two error string."""
+checks the k = 2 DAH known answer, the DAH-only call and the power-of-two error string, then
+cel_extend_batch_multi (two ctxs) and cel_extend_sharded (k = 256) as the Go Group calls them."""
 import os
 import subprocess
 
