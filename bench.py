@@ -798,6 +798,16 @@ def step_ceiling(k, probe, secs_per_square):
     }
 
 
+def _step_fields(k, probe, secs_per_square):
+    """A rider's step against its VALU floor (step_ceiling), as flat fields; none without a
+    probe of that width."""
+    step = step_ceiling(k, probe, secs_per_square) if probe else None
+    if not step:
+        return {}
+    return {"step_valu_us": step["peak"], "step_rs_transform_us": step["rs_transform_us"],
+            "step_valu_frac": step["frac"]}
+
+
 def _lib_devices(world):
     """The devices rank 0 drives in one process for the library riders: one per rank (all on
     cuda:0 in a --rehearse run, where the plan's transport is device copies)."""
@@ -1238,6 +1248,7 @@ def main():
                 "nmt_frac_sha_peak": comp5 / SHA_MEASURED_PEAK, "nmt_frac_sha_mix": comp5 / SHA_MIX_CEILING,
                 "nmt_frac_same_run": comp5 / 1e9 / probe["sha256_gcomp_per_s"] if probe else None,
                 "nmt_avg_launch_us": m5["t_com"] * 1e6,
+                **_step_fields(512, probe, t5 / (B5 * a.k512_steps)),
             }
 
         _rider(result, "k512", k512)
@@ -1252,9 +1263,7 @@ def main():
             m4 = _measure_batch(ctx, local, rank, 64, 1024 // world, a.rider_steps, 2, 4, a.input, 3, barrier,
                                 dist, dev, a.inflight)
             f = _k64_fields(world, m4["elapsed"], a.rider_steps, m4["t_ext"], m4["t_com"], 1024 // world)
-            step = step_ceiling(64, probe, m4["elapsed"] / (a.rider_steps * (1024 // world))) if probe else None
-            if step:
-                f["step_valu_us"], f["step_valu_frac"] = step["peak"], step["frac"]
+            f.update(_step_fields(64, probe, m4["elapsed"] / (a.rider_steps * (1024 // world))))
             return f
 
         _rider(result, "k64", k64)

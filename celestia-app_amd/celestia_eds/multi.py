@@ -119,11 +119,11 @@ def extend_batch_multi(ctxs, ods, want_eds=True, flags=_lib.FLAG_ORDER_CHECK):
     return eds, rr, cr, dah, st
 
 
-def probe(ctx, hbm_bytes=4 << 30, rs_k=(64, 128)):
+def probe(ctx, hbm_bytes=4 << 30, rs_k=(64, 128, 512)):
     """Same-run ceilings on ctx's device: SHA-256 G compressions/s in registers, the
     sustained shader clock over that launch (MHz), streaming-copy HBM GB/s, and the
-    microseconds of VALU one k-square's GF(2^8) extension takes with no HBM traffic
-    (`rs_transform_us_k<k>`, each k in rs_k)."""
+    microseconds of VALU one k-square's extension takes with no HBM traffic
+    (`rs_transform_us_k<k>`, each k in rs_k; GF(2^8) up to k = 128, GF(2^16) at 256 / 512)."""
     g, mhz, bw = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
     ctx.check(ctx.lib.cel_probe_sha256(ctx.handle, ctypes.byref(g), ctypes.byref(mhz)))
     ctx.check(ctx.lib.cel_probe_hbm_copy(ctx.handle, hbm_bytes, ctypes.byref(bw)))

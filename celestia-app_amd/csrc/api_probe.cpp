@@ -107,21 +107,29 @@ cel_status cel_probe_hbm_copy(cel_ctx* ctx, uint64_t bytes, double* gbps) {
 }
 
 cel_status cel_probe_rs_transform(cel_ctx* ctx, uint32_t k, double* us_per_square) {
-  if (!ctx || !us_per_square || (k != 32 && k != 64 && k != 128)) return CEL_EINVAL;
+  const bool gf16 = k == 256 || k == 512;
+  if (!ctx || !us_per_square || (k != 32 && k != 64 && k != 128 && !gf16)) return CEL_EINVAL;
   std::lock_guard<std::mutex> lock(ctx->mu);
   DeviceGuard g(ctx->device);
-  // one square's extension = 3 passes x k axes x 2 slices of 256 B; time 2^17 / k squares'
-  // worth (196,608 tiles at k = 128: ~770 waves per CU)
-  const uint32_t per_sq = 3 * k * (kShare / 256), nsq = (1u << 17) / k, ntiles = per_sq * nsq;
+  // one square's extension = 3k axis encodes (Q0 rows, then all 2k columns); a GF(2^8) tile
+  // is one 256-byte slice of an axis, a GF(2^16) tile one 64-byte Leopard block. Time about
+  // 196,608 tiles (~770 waves per CU).
+  const uint32_t per_sq = 3 * k * (kShare / (gf16 ? 64 : 256));
+  const uint32_t nsq = std::max(1u, (196608u + per_sq - 1) / per_sq), ntiles = per_sq * nsq;
+  const size_t region = gf16 ? (size_t)kShare : (size_t)k * 256;  // what every tile reads
   hipError_t e = hipSuccess;
-  uint8_t* buf = static_cast<uint8_t*>(scratch(ctx, S_AUX, (size_t)2 * k * 256, &e));
+  uint8_t* buf = static_cast<uint8_t*>(scratch(ctx, S_AUX, 2 * region, &e));
   if (!buf) return fail(ctx, CEL_ENOMEM, "device allocation failed");
-  const uint32_t* src = reinterpret_cast<const uint32_t*>(buf);
-  uint32_t* dst = reinterpret_cast<uint32_t*>(buf + (size_t)k * 256);
   hipStream_t s = ctx->stream;
-  if ((e = hipMemsetAsync(buf, 0x3C, (size_t)k * 256, s)) != hipSuccess) return hip_fail(ctx, e, "rs probe");
+  if ((e = hipMemsetAsync(buf, 0x3C, region, s)) != hipSuccess) return hip_fail(ctx, e, "rs probe");
   double secs = 0;
-  e = best_time([&] { return launch_probe_rs_transform(k, src, dst, ntiles, 0, s); }, 5, s, &secs);
+  e = best_time(
+      [&] {
+        return gf16 ? launch_probe_rs_transform_gf16(k, buf, buf + region, ntiles, s)
+                    : launch_probe_rs_transform(k, reinterpret_cast<const uint32_t*>(buf),
+                                                reinterpret_cast<uint32_t*>(buf + region), ntiles, 0, s);
+      },
+      5, s, &secs);
   if (e != hipSuccess) return hip_fail(ctx, e, "rs probe");
   *us_per_square = secs / nsq * 1e6;
   return CEL_OK;

@@ -175,6 +175,10 @@ hipError_t launch_probe_copy(const void* src, void* dst, uint64_t bytes, uint32_
 // k x 256 B of src; dst (k x 256 B) written only when store != 0.
 hipError_t launch_probe_rs_transform(uint32_t k, const uint32_t* src, uint32_t* dst, uint32_t ntiles, uint32_t store,
                                      hipStream_t s);
+// GF(2^16) register kernel alone (rs_gf16x.hip), k = 256/512: ntiles 64-byte-block tiles, all
+// loads from the 512 bytes at src, nothing stored.
+hipError_t launch_probe_rs_transform_gf16(uint32_t k, const uint8_t* src, uint8_t* dst, uint32_t ntiles,
+                                          hipStream_t s);
 
 // Repair helpers (repair_kernels.hip, nmt_kernels.hip).
 hipError_t launch_gather_axes(const uint8_t* eds, const uint8_t* mask, uint32_t W, const int32_t* idx, int is_col,

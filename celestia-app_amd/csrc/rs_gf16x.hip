@@ -351,7 +351,10 @@ __device__ __forceinline__ void pair_lo_hi(uint32_t (&w)[NW]) {
 // Tile = (square z, axis x, 64-byte column cb): one wave. Shard j of the axis sits at
 // in + z*in_sq + x*in_axis + place(j) + 64*cb (see RsGeom; blocked placement for the
 // output and the data copy when blk_log != 0).
-template <int LOGK, bool CHECK = false>
+// PROBE (cel_probe_rs_transform): the same tile whose stores run only when blk_log == 31,
+// which the probe never sets (a run-time test keeps the transform live); its geometry
+// points every load at one cache-resident 512-byte block.
+template <int LOGK, bool CHECK = false, bool PROBE = false>
 __global__ __launch_bounds__(256, LOGK == 9 ? 3 : 4) void k_rs_gf16x(RsGeom g) {
   constexpr int K = 1 << LOGK;
   constexpr int NR = K / 8;
@@ -444,13 +447,28 @@ __global__ __launch_bounds__(256, LOGK == 9 ? 3 : 4) void k_rs_gf16x(RsGeom g) {
       diff |= (v[0] ^ w[2 * i]) | (v[1] ^ w[2 * i + 1]);
     }
     if (__any(diff != 0) && lane == 0) atomicOr(g.chk_flags + (g.chk_idx ? g.chk_idx[x] : (int32_t)x), 1);
-  } else {
+  } else if (!PROBE || g.blk_log == 31u) {
 #pragma unroll
     for (int i = 0; i < NR; i++) {
       const uint32_t so = __builtin_amdgcn_readfirstlane(place(reg_bits((uint32_t)i), out_shard, out_blk));
       __builtin_amdgcn_raw_buffer_store_b64(D2{w[2 * i], w[2 * i + 1]}, rout, vout, so, 0);
     }
   }
+}
+
+// The transform alone for cel_probe_rs_transform: ntiles tiles, every load from the 512
+// bytes at src, nothing stored.
+template <int LOGK>
+static hipError_t launch_probe(const uint8_t* src, uint8_t* dst, uint32_t ntiles, hipStream_t s) {
+  RsGeom g{};
+  g.in = src;
+  g.out = dst;
+  g.n = 1u << LOGK;
+  g.len = 512;
+  g.axes = (ntiles + 7) / 8;
+  g.nsq = 1;
+  hipLaunchKernelGGL((k_rs_gf16x<LOGK, false, true>), dim3((g.axes * 8 + 3) / 4), dim3(256), 0, s, g);
+  return hipGetLastError();
 }
 
 template <int LOGK>
@@ -477,6 +495,15 @@ static bool gf16x_geom_ok(const RsGeom& g) {
   };
   return g.len % 64 == 0 && g.len > 0 && (uint64_t)g.n * g.in_shard + g.len < 0x7fffffffull &&
          span(g.out_shard, g.out_blk) < 0x7fffffffull && (!g.dcopy || span(g.dc_shard, g.dc_blk) < 0x7fffffffull);
+}
+
+hipError_t launch_probe_rs_transform_gf16(uint32_t k, const uint8_t* src, uint8_t* dst, uint32_t ntiles,
+                                          hipStream_t s) {
+  switch (k) {
+    case 256: return g16::launch_probe<8>(src, dst, ntiles, s);
+    case 512: return g16::launch_probe<9>(src, dst, ntiles, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t launch_rs_encode_gf16x(const RsGeom& g, hipStream_t s) {

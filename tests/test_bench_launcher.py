@@ -66,4 +66,7 @@ def test_step_ceiling_fields():
     assert abs(s["nmt_us"] - nmt) < 1e-9 and s["rs_transform_us"] == 7.5
     assert abs(s["peak"] - (nmt + 7.5)) < 1e-9 and abs(s["achieved"] - 45.0) < 1e-9
     assert abs(s["frac"] - (nmt + 7.5) / 45.0) < 1e-12 and s["bound"] == "valu"
-    assert bench.step_ceiling(512, probe, 1e-3) is None  # no GF(2^16) transform probe
+    assert bench.step_ceiling(512, probe, 1e-3) is None  # no k = 512 entry in this probe
+    assert bench._step_fields(512, probe, 1e-3) == {} and bench._step_fields(128, None, 1e-3) == {}
+    f = bench._step_fields(128, probe, 45e-6)
+    assert abs(f["step_valu_frac"] - s["frac"]) < 1e-12 and f["step_rs_transform_us"] == 7.5

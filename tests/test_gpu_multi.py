@@ -189,3 +189,5 @@ def test_probes(ctx):
     assert 1000 < p["hbm_copy_gbps"] < 8000
     # the transform alone at k = 128: round 2 measured 8.47 us per square (profiles/r2_gf8_transform_only.log)
     assert 4 < p["rs_transform_us_k128"] < 16 and p["rs_transform_us_k64"] < p["rs_transform_us_k128"]
+    # GF(2^16) k = 512: round 2 measured 278.5 us per square (profiles/r2_gf16_transform_only.txt)
+    assert 150 < p["rs_transform_us_k512"] < 500
