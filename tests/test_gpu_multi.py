@@ -78,7 +78,7 @@ def test_shard_plan_rccl_exchange(ctxs, oracle, k):
     plan.close()
 
 
-@pytest.mark.parametrize("k,n", [(256, 2), (256, 4), (512, 2), (512, 8)])
+@pytest.mark.parametrize("k,n", [(256, 2), (256, 4), (256, 8), (512, 2), (512, 4), (512, 8)])
 def test_shard_plan_copy_transport(ctxs, oracle, k, n):
     """N ranks as N ctxs on one device: the plan's N-rank schedule (blocked row pass,
     transpose, slab commits, record gather, finish) with device copies for the collectives;
