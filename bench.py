@@ -1104,6 +1104,24 @@ def measure_host_io(ctx, k, n=16, reps=5):
     finally:
         ctx.lib.cel_host_free(p_ods)
         ctx.lib.cel_host_free(p_eds)
+    # the same header for one k=512 block (GovMaxSquareSize, test/e2e/benchmark/throughput.go:49)
+    # on one GPU: 128 MiB of ODS over PCIe, read by the GF(2^16) row pass from page-locked memory
+    k5 = 512
+    p5, ods5 = pinned((k5, k5, 512))
+    try:
+        ods5[...] = random_ods(k5, 77)
+        rr5, cr5 = np.zeros((2 * k5, 90), np.uint8), np.zeros((2 * k5, 90), np.uint8)
+
+        def dah5():
+            ctx.check(ctx.lib.cel_extend_batch(ctx.handle, P(ods5), 1, k5, 512, None, P(rr5), P(cr5), P(dah), P(st),
+                                               _lib.FLAG_ORDER_CHECK))
+        dah5()
+        t0 = time.perf_counter()
+        for _ in range(5):
+            dah5()
+        out["single_square_k512_dah_only_ms"] = (time.perf_counter() - t0) / 5 * 1e3
+    finally:
+        ctx.lib.cel_host_free(p5)
     out["squares_per_call"] = n
     out["entry_point"] = "cel_extend_batch (host buffers, page-locked, 4 chunks over the ctx streams)"
     return out
