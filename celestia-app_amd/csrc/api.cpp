@@ -318,23 +318,26 @@ static cel_status extend_one(cel_ctx* ctx, const uint8_t* ods, uint32_t k, uint8
   const size_t ods_b = (size_t)k * k * kShare, eds_b = 4 * ods_b, roots_b = (size_t)2 * k * kNode;
   const size_t out_b = (2 * roots_b + 32 + 4 + 15) & ~(size_t)15;
   hipError_t e = hipSuccess;
-  const uint8_t* src = mapped_host(ods);
+  // The GF(2^8) row pass reads a page-locked ODS straight over PCIe (256-byte segments per
+  // shard: the upload and the row transform are one launch). The GF(2^16) row kernel reads
+  // 64-byte segments, which cross PCIe at ~39 GB/s, so at k = 256 / 512, and for pageable
+  // memory, one 2D copy puts the ODS into Q0 and the rows are extended in place (k=512 header
+  // 4.82 -> 3.58 ms, k=256 1.24 -> 1.03 ms, profiles/r5_header_gf16_dma_ab.txt).
+  const uint8_t* src = k <= kMaxGf8Width ? mapped_host(ods) : nullptr;
   uint8_t* d_eds = static_cast<uint8_t*>(scratch(ctx, S_EDS, eds_b, &e));
-  uint8_t* d_ods = src ? nullptr : static_cast<uint8_t*>(scratch(ctx, S_IN, ods_b, &e));
   uint8_t* d_work = static_cast<uint8_t*>(scratch(ctx, S_WORK, nmt_workspace_size(k, 1), &e));
   uint8_t* d_out = static_cast<uint8_t*>(scratch(ctx, S_ROOTS, out_b, &e));
   uint8_t* h_out = static_cast<uint8_t*>(host_stage(ctx, out_b));
-  if (!d_eds || (!src && !d_ods) || !d_work || !d_out || !h_out) return fail(ctx, CEL_ENOMEM, "allocation failed");
+  if (!d_eds || !d_work || !d_out || !h_out) return fail(ctx, CEL_ENOMEM, "allocation failed");
   uint8_t* h_dev = const_cast<uint8_t*>(mapped_host(h_out));
   if (!h_dev) return fail(ctx, CEL_EDEVICE, "page-locked staging is not mapped for the device");
   int32_t* d_st = reinterpret_cast<int32_t*>(d_out + 2 * roots_b + 32);
   hipStream_t s = ctx->stream, d = ctx->dl[0];
   auto enqueue = [&]() -> hipError_t {
     hipError_t r;
-    if (!src) {
-      if ((r = hipMemcpyAsync(d_ods, ods, ods_b, hipMemcpyHostToDevice, s)) != hipSuccess) return r;
-      src = d_ods;
-    }
+    if (!src && (r = hipMemcpy2DAsync(d_eds, (size_t)2 * k * kShare, ods, (size_t)k * kShare, (size_t)k * kShare, k,
+                                      hipMemcpyHostToDevice, s)) != hipSuccess)
+      return r;
     if ((r = launch_extend_rows(d_eds, k, 0, k, ctx->tables, s, src)) != hipSuccess ||
         (r = launch_extend_cols(d_eds, k, 1, ctx->tables, s)) != hipSuccess)
       return r;
