@@ -321,8 +321,8 @@ static cel_status extend_one(cel_ctx* ctx, const uint8_t* ods, uint32_t k, uint8
   // The GF(2^8) row pass reads a page-locked ODS straight over PCIe (256-byte segments per
   // shard: the upload and the row transform are one launch). The GF(2^16) row kernel reads
   // 64-byte segments, which cross PCIe at ~39 GB/s, so at k = 256 / 512, and for pageable
-  // memory, one 2D copy puts the ODS into Q0 and the rows are extended in place (k=512 header
-  // 4.82 -> 3.58 ms, k=256 1.24 -> 1.03 ms, profiles/r5_header_gf16_dma_ab.txt).
+  // memory, DMA copies put the ODS into Q0 and the rows are extended in place (k=512 header
+  // 4.82 -> 3.43 ms, k=256 1.24 -> 1.03 ms, profiles/r5_header_gf16_dma_ab.txt).
   const uint8_t* src = k <= kMaxGf8Width ? mapped_host(ods) : nullptr;
   uint8_t* d_eds = static_cast<uint8_t*>(scratch(ctx, S_EDS, eds_b, &e));
   uint8_t* d_work = static_cast<uint8_t*>(scratch(ctx, S_WORK, nmt_workspace_size(k, 1), &e));
@@ -335,24 +335,48 @@ static cel_status extend_one(cel_ctx* ctx, const uint8_t* ods, uint32_t k, uint8
   hipStream_t s = ctx->stream, d = ctx->dl[0];
   auto enqueue = [&]() -> hipError_t {
     hipError_t r;
-    if (!src && (r = hipMemcpy2DAsync(d_eds, (size_t)2 * k * kShare, ods, (size_t)k * kShare, (size_t)k * kShare, k,
-                                      hipMemcpyHostToDevice, s)) != hipSuccess)
-      return r;
-    if ((r = launch_extend_rows(d_eds, k, 0, k, ctx->tables, s, src)) != hipSuccess ||
-        (r = launch_extend_cols(d_eds, k, 1, ctx->tables, s)) != hipSuccess)
-      return r;
+    const bool order = (flags & CEL_FLAG_ORDER_CHECK) != 0;
+    const size_t rowb = (size_t)2 * k * kShare, odsrow = (size_t)k * kShare;
+    uint32_t leaf0 = 0;  // EDS rows whose leaves are hashed already
+    if (k == 512 && mapped_host(ods)) {
+      // One k=512 block from page-locked memory: 128 MiB crosses PCIe in 4 row chunks on a
+      // copy stream, and each chunk's rows are extended and their leaves hashed on the
+      // compute stream while the next one crosses (3.58 -> 3.43 ms; at k = 256 the chunks
+      // cost more than they hide: profiles/r5_header_gf16_dma_ab.txt). The push-order check
+      // of a chunk's first row reads the row above, which the previous chunk brought.
+      constexpr uint32_t kUp = 4;
+      const uint32_t rows = k / kUp;
+      hipStream_t cp = ctx->dl[1];
+      if ((r = hipEventRecord(ctx->ev_start, s)) != hipSuccess || (r = hipStreamWaitEvent(cp, ctx->ev_start, 0)))
+        return r;
+      for (uint32_t c = 0; c < kUp; c++) {
+        const uint32_t r0 = c * rows;
+        if ((r = hipMemcpy2DAsync(d_eds + r0 * rowb, rowb, ods + r0 * odsrow, odsrow, odsrow, rows,
+                                  hipMemcpyHostToDevice, cp)) != hipSuccess ||
+            (r = hipEventRecord(ctx->ev_done[c], cp)) != hipSuccess ||
+            (r = hipStreamWaitEvent(s, ctx->ev_done[c], 0)) != hipSuccess ||
+            (r = launch_extend_rows(d_eds, k, r0, r0 + rows, ctx->tables, s)) != hipSuccess ||
+            (r = launch_commit_leaves(d_eds, k, 1, d_work, order, r0, r0 + rows, c == 0, s)) != hipSuccess)
+          return r;
+      }
+      leaf0 = k;
+    } else {
+      if (!src && (r = hipMemcpy2DAsync(d_eds, rowb, ods, odsrow, odsrow, k, hipMemcpyHostToDevice, s)) != hipSuccess)
+        return r;
+      if ((r = launch_extend_rows(d_eds, k, 0, k, ctx->tables, s, src)) != hipSuccess) return r;
+    }
+    if ((r = launch_extend_cols(d_eds, k, 1, ctx->tables, s)) != hipSuccess) return r;
     if (eds_out &&
         ((r = hipEventRecord(ctx->ev_rs[0], s)) != hipSuccess || (r = hipStreamWaitEvent(d, ctx->ev_rs[0], 0))))
       return r;
     // the DAH launch writes every result into the page-locked staging itself
-    if ((r = launch_commit_leaves(d_eds, k, 1, d_work, (flags & CEL_FLAG_ORDER_CHECK) != 0, 0, 2 * k, true, s)) !=
-            hipSuccess ||
+    if ((r = launch_commit_leaves(d_eds, k, 1, d_work, order, leaf0, 2 * k, leaf0 == 0, s)) != hipSuccess ||
         (r = launch_commit_trees(k, 1, d_out, d_out + roots_b, d_out + 2 * roots_b, d_st, d_work, s, h_dev,
                                  (uint32_t)out_b)) != hipSuccess)
       return r;
     if (eds_out) {
       // after every kernel is enqueued: a copy into pageable memory blocks the calling thread
-      const size_t rowb = (size_t)2 * k * kShare, half = (size_t)k * kShare;
+      const size_t half = (size_t)k * kShare;
       r = (flags & CEL_FLAG_PARITY_ONLY)
               ? hipMemcpy2DAsync(eds_out + half, rowb, d_eds + half, rowb, half, k, hipMemcpyDeviceToHost, d)
               : hipMemcpyAsync(eds_out, d_eds, k * rowb, hipMemcpyDeviceToHost, d);

@@ -132,6 +132,59 @@ def test_gf16_square_k256(ctx, oracle):
     assert dev._dah == dah
 
 
+def _pinned(ctx, shape):
+    import ctypes
+    nbytes = int(np.prod(shape))
+    p = ctx.lib.cel_host_alloc(nbytes)
+    assert p, "cel_host_alloc failed"
+    return p, np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p)).reshape(shape)
+
+
+@pytest.mark.parametrize("k", [256, 512])
+def test_pinned_single_square_gf16(ctx, oracle, k):
+    """One square from page-locked memory at the GF(2^16) widths (cel_extend_batch, n = 1):
+    the ODS goes up by DMA into Q0 (at k = 512 in four row chunks whose rows and leaves are
+    processed while the next chunk crosses PCIe). Full EDS, parity only and roots only
+    against the oracle; a push-order violation between the rows on either side of a chunk
+    boundary (rows 127 / 128) is reported with the reference's error."""
+    import ctypes
+    from celestia_eds import CelError, _lib
+    ods_ref = random_ods(k, 600 + k)
+    e_ref, rr_ref, cr_ref, dah_ref = oracle.extend_and_commit(ods_ref)
+    w = 2 * k
+    p_ods, ods = _pinned(ctx, (k, k, 512))
+    p_eds, eds = _pinned(ctx, (w, w, 512))
+    P = lambda x: x.ctypes.data_as(ctypes.c_void_p)
+    rr, cr, dah, st = np.zeros((w, 90), np.uint8), np.zeros((w, 90), np.uint8), np.zeros(32, np.uint8), np.zeros(1, np.int32)
+    try:
+        ods[...] = ods_ref
+        for fl, want_eds in ((0, True), (_lib.FLAG_PARITY_ONLY, True), (0, False)):
+            eds[...] = 0
+            ctx.check(ctx.lib.cel_extend_batch(ctx.handle, ctypes.c_void_p(p_ods), 1, k, 512,
+                                               ctypes.c_void_p(p_eds) if want_eds else None, P(rr), P(cr), P(dah),
+                                               P(st), _lib.FLAG_ORDER_CHECK | fl))
+            assert np.array_equal(rr, rr_ref) and np.array_equal(cr, cr_ref) and dah.tobytes() == dah_ref
+            if want_eds:
+                got = eds.copy()
+                if fl:
+                    assert not got[:k, :k].any(), "Q0 written under CEL_FLAG_PARITY_ONLY"
+                    got[:k, :k] = ods_ref
+                assert np.array_equal(got, e_ref), "EDS differs"
+        # column order broken only across the chunk boundary: row 128 takes row 0's
+        # namespaces (still sorted along the row, below row 127's in every column)
+        bad = ods_ref.copy()
+        bad[128, :, :29] = bad[0, :, :29]
+        assert (bad[128, :, :29].tobytes() < bad[127, :, :29].tobytes())
+        ods[...] = bad
+        with pytest.raises(CelError) as e:
+            ctx.check(ctx.lib.cel_extend_batch(ctx.handle, ctypes.c_void_p(p_ods), 1, k, 512, None, P(rr), P(cr),
+                                               P(dah), P(st), _lib.FLAG_ORDER_CHECK))
+        assert e.value.status == _lib.EORDER
+    finally:
+        ctx.lib.cel_host_free(p_ods)
+        ctx.lib.cel_host_free(p_eds)
+
+
 def test_gf16_square_k512(ctx, oracle):
     """k = 512 (config 3's square, here on one GPU): GF(2^16) register kernel, 2k = 1024
     trees. Roots, DAH and the EDS bytes (by digest) against the oracle restatement."""
