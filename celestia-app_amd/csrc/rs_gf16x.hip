@@ -130,6 +130,16 @@ __device__ __forceinline__ Tb lane_tab(uint32_t m0, uint32_t m1, uint32_t m2) {
             f(a.t2, b.t2, c.t2)};
 }
 
+// lane_tab of this lane, its masks recomputed from the lane id where the layer starts (three
+// lane masks live across the whole transform pushed the k = 512 kernel into scratch spills)
+template <int S>
+__device__ __forceinline__ Tb lane_tab_here() {
+  uint32_t l = threadIdx.x;
+  asm volatile("" : "+v"(l));
+  const uint32_t L = (l & 63u) >> 3;
+  return lane_tab<S>(0u - (L & 1u), 0u - ((L >> 1) & 1u), 0u - ((L >> 2) & 1u));
+}
+
 // Register index r (arrangement A) -> the register-held bits of the shard index.
 template <int LOGK>
 constexpr uint32_t shard_bits_a(uint32_t r) {
@@ -411,15 +421,12 @@ __global__ __launch_bounds__(256, LOGK == 9 ? 3 : 4) void k_rs_gf16x(RsGeom g) {
   }
   pair_lo_hi(w);
   convert(w, m7, m3);  // -> (a, b)
-  // lane masks of the bits of L
-  const uint32_t mk0 = (L & 1u) ? 0xFFFFFFFFu : 0u, mk1 = (L & 2u) ? 0xFFFFFFFFu : 0u,
-                 mk2 = (L & 4u) ? 0xFFFFFFFFu : 0u;
   // IFFT, arrangement A
-  layer_a<LOGK, 0, true>(w, lane_tab<5>(mk0, mk1, mk2), m7, m3);
-  layer_a<LOGK, 1, true>(w, lane_tab<4>(mk0, mk1, mk2), m7, m3);
-  layer_a<LOGK, 2, true>(w, lane_tab<3>(mk0, mk1, mk2), m7, m3);
-  layer_a<LOGK, 3, true>(w, lane_tab<2>(mk0, mk1, mk2), m7, m3);
-  layer_a<LOGK, 4, true>(w, lane_tab<1>(mk0, mk1, mk2), m7, m3);
+  layer_a<LOGK, 0, true>(w, lane_tab_here<5>(), m7, m3);
+  layer_a<LOGK, 1, true>(w, lane_tab_here<4>(), m7, m3);
+  layer_a<LOGK, 2, true>(w, lane_tab_here<3>(), m7, m3);
+  layer_a<LOGK, 3, true>(w, lane_tab_here<2>(), m7, m3);
+  layer_a<LOGK, 4, true>(w, lane_tab_here<1>(), m7, m3);
   swap_bit<2>(w);
   swap_bit<3>(w);
   swap_bit<4>(w);
@@ -428,16 +435,21 @@ __global__ __launch_bounds__(256, LOGK == 9 ? 3 : 4) void k_rs_gf16x(RsGeom g) {
   swap_bit<3>(w);
   swap_bit<4>(w);
   // FFT, arrangement A
-  layer_a<LOGK, 4, false>(w, lane_tab<1>(mk0, mk1, mk2), m7, m3);
-  layer_a<LOGK, 3, false>(w, lane_tab<2>(mk0, mk1, mk2), m7, m3);
-  layer_a<LOGK, 2, false>(w, lane_tab<3>(mk0, mk1, mk2), m7, m3);
-  layer_a<LOGK, 1, false>(w, lane_tab<4>(mk0, mk1, mk2), m7, m3);
-  layer_a<LOGK, 0, false>(w, lane_tab<5>(mk0, mk1, mk2), m7, m3);
+  layer_a<LOGK, 4, false>(w, lane_tab_here<1>(), m7, m3);
+  layer_a<LOGK, 3, false>(w, lane_tab_here<2>(), m7, m3);
+  layer_a<LOGK, 2, false>(w, lane_tab_here<3>(), m7, m3);
+  layer_a<LOGK, 1, false>(w, lane_tab_here<4>(), m7, m3);
+  layer_a<LOGK, 0, false>(w, lane_tab_here<5>(), m7, m3);
   convert(w, m7, m3);  // -> (lo, hi)
   pair_lo_hi(w);
   const auto rout = rsrc(g.out + (uint64_t)z * g.out_sq + (uint64_t)xa * g.out_axis);
   const uint32_t out_shard = (uint32_t)g.out_shard, out_blk = (uint32_t)g.out_blk;
-  const uint32_t vout = place(lane_bits, out_shard, out_blk) + col;
+  // the lane's output offset from the lane id again: col and lane_bits held across the
+  // transform would cost two more VGPRs at the 168 the kernel runs at
+  uint32_t ln = threadIdx.x;
+  asm volatile("" : "+v"(ln));
+  ln &= 63u;
+  const uint32_t vout = place((ln >> 3) << 5, out_shard, out_blk) + cb * 64u + (ln & 7u) * 8u;
   if constexpr (CHECK) {  // repair's encoding check: compare with the parity in place
     uint32_t diff = 0;
 #pragma unroll
