@@ -24,6 +24,7 @@ import "C"
 import (
 	"errors"
 	"fmt"
+	"runtime"
 	"sync"
 	"unsafe"
 
@@ -99,6 +100,68 @@ func squareWidth(n int) int {
 type Context struct {
 	mu  sync.Mutex
 	ctx *C.cel_ctx
+	// Page-locked staging for an ODS (cel_host_alloc, grown on demand, used under mu). The
+	// library's one-square path reads page-locked input straight over PCIe (k <= 128) or
+	// uploads it in chunks beside the row pass (k = 512); from ordinary memory the same
+	// header takes 5-10 % longer (profiles/r5_header_pageable_ods.txt).
+	stage    unsafe.Pointer
+	stageLen int
+}
+
+// stagedLocked copies shares into the page-locked staging buffer and returns it, or a
+// C.malloc'd copy (release != nil: the caller frees it) when page-locked memory is not to
+// be had. The caller holds c.mu.
+func (c *Context) stagedLocked(shares [][]byte) (buf unsafe.Pointer, release func()) {
+	need := len(shares) * ShareSize
+	if c.stageLen < need {
+		if c.stage != nil {
+			C.cel_host_free(c.stage)
+		}
+		c.stage, c.stageLen = C.cel_host_alloc(C.size_t(need)), need
+		if c.stage == nil {
+			c.stageLen = 0
+		}
+	}
+	buf = c.stage
+	if buf == nil {
+		buf = C.malloc(C.size_t(need))
+		release = func() { C.free(buf) }
+	}
+	dst := unsafe.Slice((*byte)(buf), need)
+	copyShares(dst, shares)
+	return buf, release
+}
+
+// copyShares flattens shares into dst, split over up to 8 goroutines for a large square
+// (one core copies ~8 MiB, a k = 128 ODS, in about as long as the device takes for the
+// whole header).
+func copyShares(dst []byte, shares [][]byte) {
+	parts := runtime.GOMAXPROCS(0)
+	if parts > 8 {
+		parts = 8
+	}
+	if len(dst) < 4<<20 || parts < 2 {
+		for i, s := range shares {
+			copy(dst[i*ShareSize:], s)
+		}
+		return
+	}
+	var wg sync.WaitGroup
+	per := (len(shares) + parts - 1) / parts
+	for lo := 0; lo < len(shares); lo += per {
+		hi := lo + per
+		if hi > len(shares) {
+			hi = len(shares)
+		}
+		wg.Add(1)
+		go func(lo, hi int) {
+			defer wg.Done()
+			for i := lo; i < hi; i++ {
+				copy(dst[i*ShareSize:], shares[i])
+			}
+		}(lo, hi)
+	}
+	wg.Wait()
 }
 
 func NewContext(device int) (*Context, error) {
@@ -109,7 +172,15 @@ func NewContext(device int) (*Context, error) {
 	return &Context{ctx: c}, nil
 }
 
-func (c *Context) Close() { C.cel_ctx_destroy(c.ctx) }
+func (c *Context) Close() {
+	c.mu.Lock()
+	defer c.mu.Unlock()
+	if c.stage != nil {
+		C.cel_host_free(c.stage)
+		c.stage, c.stageLen = nil, 0
+	}
+	C.cel_ctx_destroy(c.ctx)
+}
 
 // call runs f (a cel_* call on c.ctx) under c.mu and turns its status into an error,
 // reading cel_last_error before the lock is released (another goroutine's call on the
@@ -148,22 +219,20 @@ func (c *Context) ExtendShares(shares [][]byte) (flat []byte, rowRoots, colRoots
 func (c *Context) extend(shares [][]byte, flags C.uint32_t) (flat []byte, rowRoots, colRoots [][]byte, dah []byte,
 	err error) {
 	n := len(shares)
-	buf := C.malloc(C.size_t(n * ShareSize))
-	defer C.free(buf)
-	dst := unsafe.Slice((*byte)(buf), n*ShareSize)
-	for i, s := range shares {
-		copy(dst[i*ShareSize:], s)
-	}
 	w := 2 * squareWidth(n)
 	flat = make([]byte, w*w*ShareSize)
 	rr := make([]byte, w*NmtNodeSize)
 	cr := make([]byte, w*NmtNodeSize)
 	dah = make([]byte, 32)
-	err = c.call(func() C.cel_status {
-		return C.cel_extend_shares(c.ctx, (*C.uint8_t)(buf), C.uint32_t(n), ShareSize,
-			(*C.uint8_t)(unsafe.Pointer(&flat[0])), (*C.uint8_t)(unsafe.Pointer(&rr[0])),
-			(*C.uint8_t)(unsafe.Pointer(&cr[0])), (*C.uint8_t)(unsafe.Pointer(&dah[0])), flags)
-	})
+	c.mu.Lock()
+	buf, release := c.stagedLocked(shares)
+	err = c.errLocked(C.cel_extend_shares(c.ctx, (*C.uint8_t)(buf), C.uint32_t(n), ShareSize,
+		(*C.uint8_t)(unsafe.Pointer(&flat[0])), (*C.uint8_t)(unsafe.Pointer(&rr[0])),
+		(*C.uint8_t)(unsafe.Pointer(&cr[0])), (*C.uint8_t)(unsafe.Pointer(&dah[0])), flags))
+	c.mu.Unlock()
+	if release != nil {
+		release()
+	}
 	if err != nil {
 		return nil, nil, nil, nil, err
 	}
@@ -239,21 +308,19 @@ func (c *Context) DataAvailabilityHeader(shares [][]byte, codec rsmt2d.Codec) (r
 	if !deviceCodec(codec) || !deviceShares(shares) {
 		return reference()
 	}
-	buf := C.malloc(C.size_t(n * ShareSize))
-	defer C.free(buf)
-	dst := unsafe.Slice((*byte)(buf), n*ShareSize)
-	for i, s := range shares {
-		copy(dst[i*ShareSize:], s)
-	}
 	w := 2 * k
 	rr := make([]byte, w*NmtNodeSize)
 	cr := make([]byte, w*NmtNodeSize)
 	dah := make([]byte, 32)
-	err = c.call(func() C.cel_status {
-		return C.cel_extend_shares(c.ctx, (*C.uint8_t)(buf), C.uint32_t(n), ShareSize, nil,
-			(*C.uint8_t)(unsafe.Pointer(&rr[0])), (*C.uint8_t)(unsafe.Pointer(&cr[0])),
-			(*C.uint8_t)(unsafe.Pointer(&dah[0])), flagOrder)
-	})
+	c.mu.Lock()
+	buf, release := c.stagedLocked(shares)
+	err = c.errLocked(C.cel_extend_shares(c.ctx, (*C.uint8_t)(buf), C.uint32_t(n), ShareSize, nil,
+		(*C.uint8_t)(unsafe.Pointer(&rr[0])), (*C.uint8_t)(unsafe.Pointer(&cr[0])),
+		(*C.uint8_t)(unsafe.Pointer(&dah[0])), flagOrder))
+	c.mu.Unlock()
+	if release != nil {
+		release()
+	}
 	if tooBig(err) {
 		return reference()
 	}

@@ -1,7 +1,7 @@
 """One square's header through the host entry point (cel_extend_batch, n = 1, eds_out = NULL,
 page-locked ODS): ms per call at k = 128, 256, 512 and the DAH (dev aid; CEL_EDS_LIB picks a
 library build, so variants can be compared on one box):
-  python tools/header_lat.py [reps]"""
+  python tools/header_lat.py [reps] [pageable]   (pageable: the ODS in ordinary host memory)"""
 import ctypes
 import os
 import sys
@@ -16,13 +16,18 @@ from celestia_eds import _lib, default_context  # noqa: E402
 from celestia_eds.testfactory import random_ods  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+pageable = len(sys.argv) > 2 and sys.argv[2] == "pageable"
 ctx = default_context(0)
 P = lambda x: x.ctypes.data_as(ctypes.c_void_p)
 for k in (128, 256, 512):
     nbytes = k * k * 512
-    p = ctx.lib.cel_host_alloc(nbytes)
-    ods = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p)).reshape(k, k, 512)
-    ods[...] = random_ods(k, 31 + k)
+    if pageable:
+        ods = np.ascontiguousarray(random_ods(k, 31 + k))
+        p = ods.ctypes.data
+    else:
+        p = ctx.lib.cel_host_alloc(nbytes)
+        ods = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p)).reshape(k, k, 512)
+        ods[...] = random_ods(k, 31 + k)
     rr, cr = np.zeros((2 * k, 90), np.uint8), np.zeros((2 * k, 90), np.uint8)
     dah, st = np.zeros(32, np.uint8), np.zeros(1, np.int32)
 
@@ -36,4 +41,5 @@ for k in (128, 256, 512):
         call()
     ms = (time.perf_counter() - t0) / reps * 1e3
     print(f"k={k:4d}: {ms:7.3f} ms per header  dah {dah.tobytes().hex()[:16]}", flush=True)
-    ctx.lib.cel_host_free(p)
+    if not pageable:
+        ctx.lib.cel_host_free(p)
