@@ -87,18 +87,18 @@ func (g *Group) ExtendSquare(shares [][]byte, codec rsmt2d.Codec) (*rsmt2d.Exten
 		}
 		return rsmt2d.ComputeExtendedDataSquare(shares, codec, wrapper.NewConstructor(uint64(k)))
 	}
-	buf := C.malloc(C.size_t(n * ShareSize))
-	defer C.free(buf)
-	dst := unsafe.Slice((*byte)(buf), n*ShareSize)
-	for i, s := range shares {
-		copy(dst[i*ShareSize:], s)
-	}
 	w := 2 * k
 	flat := make([]byte, w*w*ShareSize)
 	rr := make([]byte, w*NmtNodeSize)
 	cr := make([]byte, w*NmtNodeSize)
 	dah := make([]byte, 32)
 	arr, release := g.handles()
+	// the first Context's page-locked staging (its lock is held): the per-device row blocks
+	// go up by DMA from page-locked memory
+	buf, rel := g.Ctxs[0].stagedLocked(shares)
+	if rel != nil {
+		defer rel()
+	}
 	st := C.cel_extend_sharded(arr, C.uint32_t(len(g.Ctxs)), (*C.uint8_t)(buf), C.uint32_t(k), ShareSize,
 		(*C.uint8_t)(unsafe.Pointer(&flat[0])), (*C.uint8_t)(unsafe.Pointer(&rr[0])),
 		(*C.uint8_t)(unsafe.Pointer(&cr[0])), (*C.uint8_t)(unsafe.Pointer(&dah[0])), flagOrder|flagParity)
@@ -146,19 +146,19 @@ func (g *Group) DataAvailabilityHeaders(squares [][][]byte) (rowRoots, colRoots 
 	}
 	k := squareWidth(n)
 	m := len(squares)
-	buf := C.malloc(C.size_t(m * n * ShareSize))
-	defer C.free(buf)
-	dst := unsafe.Slice((*byte)(buf), m*n*ShareSize)
-	for j, sq := range squares {
-		for i, s := range sq {
-			copy(dst[(j*n+i)*ShareSize:], s)
-		}
+	all := make([][]byte, 0, m*n)
+	for _, sq := range squares {
+		all = append(all, sq...)
 	}
 	w := 2 * k
 	rr := make([]byte, m*w*NmtNodeSize)
 	cr := make([]byte, m*w*NmtNodeSize)
 	dah := make([]byte, m*32)
 	arr, release := g.handles()
+	buf, rel := g.Ctxs[0].stagedLocked(all) // page-locked: every chunk's upload is a plain DMA
+	if rel != nil {
+		defer rel()
+	}
 	st := C.cel_extend_batch_multi(arr, C.uint32_t(len(g.Ctxs)), (*C.uint8_t)(buf), C.uint32_t(m), C.uint32_t(k),
 		ShareSize, nil, (*C.uint8_t)(unsafe.Pointer(&rr[0])), (*C.uint8_t)(unsafe.Pointer(&cr[0])),
 		(*C.uint8_t)(unsafe.Pointer(&dah[0])), nil, flagOrder)
