@@ -165,6 +165,31 @@ def test_extend_batch_multi_two_ctxs(ctxs, oracle, k, n, g):
         assert dah[i].tobytes() == w_dah
 
 
+@pytest.mark.parametrize("k,n,g", [(64, 5, 4), (128, 3, 2), (32, 6, 4)])
+def test_extend_batch_multi_pinned_ods(ctxs, oracle, k, n, g):
+    """cel_extend_batch_multi over an ODS batch in page-locked memory (cel_host_alloc, as
+    the Go shim stages it): the parts that get one square take api.cpp's one-square path
+    (the GF(2^8) row pass reading the mapped host pages), the others the batch upload.
+    Every square against the oracle."""
+    import ctypes
+    from celestia_eds.multi import extend_batch_multi
+    c0 = ctxs[0]
+    nbytes = n * k * k * 512
+    p = c0.lib.cel_host_alloc(nbytes)
+    assert p, "cel_host_alloc failed"
+    try:
+        ods = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p)).reshape(n, k, k, 512)
+        ods[...] = np.stack([random_ods(k, 980 + i) for i in range(n)])
+        eds, rr, cr, dah, st = extend_batch_multi(ctxs[:g], ods)
+        assert (st == 0).all()
+        for i in range(n):
+            w_eds, w_rr, w_cr, w_dah = oracle.extend_and_commit(np.array(ods[i]))
+            assert np.array_equal(eds[i], w_eds) and np.array_equal(rr[i], w_rr) and np.array_equal(cr[i], w_cr)
+            assert dah[i].tobytes() == w_dah
+    finally:
+        c0.lib.cel_host_free(p)
+
+
 def test_extend_batch_multi_status(ctxs):
     """A bad square in the second ctx's range: its status is CEL_EORDER, the others 0, and the
     call returns CEL_EORDER with the reference's message."""

@@ -140,13 +140,16 @@ def _pinned(ctx, shape):
     return p, np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p)).reshape(shape)
 
 
-@pytest.mark.parametrize("k", [256, 512])
-def test_pinned_single_square_gf16(ctx, oracle, k):
-    """One square from page-locked memory at the GF(2^16) widths (cel_extend_batch, n = 1):
+@pytest.mark.parametrize("k", [32, 64, 128, 256, 512])
+def test_pinned_single_square(ctx, oracle, k):
+    """One square from page-locked memory (cel_extend_batch, n = 1). At the GF(2^16) widths
     the ODS goes up by DMA into Q0 (at k = 512 in four row chunks whose rows and leaves are
-    processed while the next chunk crosses PCIe). Full EDS, parity only and roots only
-    against the oracle; a push-order violation between the rows on either side of a chunk
-    boundary (rows 127 / 128) is reported with the reference's error."""
+    processed while the next chunk crosses PCIe); at k = 32..128 the GF(2^8) row pass reads
+    the ODS straight from the mapped host pages and the top rows download early into the
+    page-locked EDS (api.cpp's one-square path, which the Go shim's staged ODS always
+    takes). Full EDS, parity only and roots only against the oracle; a push-order
+    violation between the rows on either side of a chunk boundary (rows 127 / 128; k / 2
+    - 1 / k / 2 below k = 256) is reported with the reference's error."""
     import ctypes
     from celestia_eds import CelError, _lib
     ods_ref = random_ods(k, 600 + k)
@@ -172,9 +175,10 @@ def test_pinned_single_square_gf16(ctx, oracle, k):
                 assert np.array_equal(got, e_ref), "EDS differs"
         # column order broken only across the chunk boundary: row 128 takes row 0's
         # namespaces (still sorted along the row, below row 127's in every column)
+        b = 128 if k >= 256 else k // 2
         bad = ods_ref.copy()
-        bad[128, :, :29] = bad[0, :, :29]
-        assert (bad[128, :, :29].tobytes() < bad[127, :, :29].tobytes())
+        bad[b, :, :29] = bad[0, :, :29]
+        assert (bad[b, :, :29].tobytes() < bad[b - 1, :, :29].tobytes())
         ods[...] = bad
         with pytest.raises(CelError) as e:
             ctx.check(ctx.lib.cel_extend_batch(ctx.handle, ctypes.c_void_p(p_ods), 1, k, 512, None, P(rr), P(cr),
@@ -487,9 +491,10 @@ def test_batches_in_flight_on_two_streams(ctx, oracle, k, n):
 
 
 def test_bench_shape_batches_in_flight(ctx, oracle):
-    """The bench's full shape (BASELINE config 2): 256 k=128 squares per batch, two
-    batches in flight on two caller streams (CEL_FLAG_CALLER_STREAM, bench --inflight 2),
-    steps alternating. Size-independent properties against the oracle: every square's
+    """The bench's batch shape (BASELINE config 2) through the raw C ABI: 256 k=128
+    squares per batch, two batches in flight on two caller streams (CEL_FLAG_CALLER_STREAM),
+    steps alternating (the bench's default four batches through SquareBatch:
+    tests/test_gpu_bench_shapes.py). Size-independent properties against the oracle: every square's
     DAH and its 512 roots equal those of its source (4 distinct ODSs, as the bench
     replicates them), a sampled square's whole EDS is bit-exact, and every status is 0."""
     import ctypes

@@ -52,6 +52,17 @@
 #define I_ADD_BANK0(d) "v_add_u32 " d ", v64, v68\n"
 #define I_LSHR(d) "v_lshrrev_b32 " d ", 7, v64\n"
 #define I_ALIGN_SGPR(d) "v_alignbit_b32 " d ", v64, s20, 7\n"
+// round 6: the GF(2^8) v_perm product's operand forms (table dword in an SGPR and a VGPR,
+// selector in a VGPR) and the bit-sliced network's xor3 with an SGPR
+#define I_PERM_SVV_BANKS(d) "v_perm_b32 " d ", s20, v64, v65\n"
+#define I_PERM_SVV_BANK0(d) "v_perm_b32 " d ", s20, v64, v68\n"
+#define I_PERM_VVV_BANKS(d) "v_perm_b32 " d ", v64, v65, v66\n"
+#define I_PERM_VVV_BANK0(d) "v_perm_b32 " d ", v64, v68, v72\n"
+#define I_PERM_0SV(d) "v_perm_b32 " d ", 0, s20, v64\n"
+#define I_BITOP3_VSV_BANKS(d) "v_bitop3_b32 " d ", v64, s20, v65 bitop3:0x96\n"
+#define I_AND_SV(d) "v_and_b32 " d ", s20, v64\n"
+#define I_BFI_VSV_BANKS(d) "v_bitop3_b32 " d ", s20, v64, v65 bitop3:0xCA\n"
+#define I_PERM_VVS_BANKS(d) "v_perm_b32 " d ", v64, v65, s20\n"
 
 #define KERNEL(NAME, I)                                                                                      \
   __global__ __launch_bounds__(256) void NAME(uint32_t* out, int iters) {                                 \
@@ -82,6 +93,15 @@ KERNEL(k_bitop3_2bank, I_BITOP3_2BANK)
 KERNEL(k_bitop3_sgpr, I_BITOP3_SGPR)
 KERNEL(k_xor_bank0, I_XOR_BANK0)
 KERNEL(k_add_bank0, I_ADD_BANK0)
+KERNEL(k_perm_svv_banks, I_PERM_SVV_BANKS)
+KERNEL(k_perm_svv_bank0, I_PERM_SVV_BANK0)
+KERNEL(k_perm_vvv_banks, I_PERM_VVV_BANKS)
+KERNEL(k_perm_vvv_bank0, I_PERM_VVV_BANK0)
+KERNEL(k_perm_0sv, I_PERM_0SV)
+KERNEL(k_bitop3_vsv_banks, I_BITOP3_VSV_BANKS)
+KERNEL(k_and_sv, I_AND_SV)
+KERNEL(k_bfi_svv_banks, I_BFI_VSV_BANKS)
+KERNEL(k_perm_vvs_banks, I_PERM_VVS_BANKS)
 
 typedef void (*kfn)(uint32_t*, int);
 
@@ -99,7 +119,7 @@ static void run(const char* name, kfn k, uint32_t* out, int wg_per_cu) {
   CK(hipEventElapsedTime(&ms, a, b));
   const double winst = (double)blocks * 4 * iters * 64;  // wave-instructions
   // cycles per wave-instruction per SIMD at 2.4 GHz (1024 SIMDs)
-  printf("%-16s waves/SIMD %2d  %8.3f ms  %7.2f T lane-ops/s  %5.2f cycles per wave64 instruction @2.4GHz\n", name,
+  printf("%-18s waves/SIMD %2d  %8.3f ms  %7.2f T lane-ops/s  %5.2f cycles per wave64 instruction @2.4GHz\n", name,
          wg_per_cu, ms, winst * 64 / (ms * 1e-3) / 1e12, ms * 1e-3 * 2.4e9 * 1024 / winst);
 }
 
@@ -125,7 +145,16 @@ int main(int argc, char** argv) {
             {"bitop3 2 banks", k_bitop3_2bank},
             {"bitop3 v,s,v b0", k_bitop3_sgpr},
             {"xor bank0", k_xor_bank0},
-            {"add_u32 bank0", k_add_bank0}};
+            {"add_u32 bank0", k_add_bank0},
+            {"perm s,v,v banks", k_perm_svv_banks},
+            {"perm s,v,v bank0", k_perm_svv_bank0},
+            {"perm v,v,v banks", k_perm_vvv_banks},
+            {"perm v,v,v bank0", k_perm_vvv_bank0},
+            {"perm 0,s,v", k_perm_0sv},
+            {"perm v,v,s banks", k_perm_vvs_banks},
+            {"bitop3 v,s,v bnks", k_bitop3_vsv_banks},
+            {"bfi s,v,v banks", k_bfi_svv_banks},
+            {"and s,v", k_and_sv}};
   for (int w : {2, 4})
     for (auto& k : ks) run(k.n, k.k, out, w);
   return 0;
