@@ -855,12 +855,18 @@ def measure_rowshard_lib(k, world, steps, warmup, depth):
 
     t1 = clock(one, steps)
     tp = clock(piped, steps)
-    transport = p0.transport
+    transport, note = p0.transport, p0.note
+    a2a_us = p0.time_exchange(10)  # the all-to-all alone (None at one rank in place)
     for p in plans:
         p.close()
-    return {"workload": f"config 3: one k={k} square row-sharded over {len(devs)} GPU(s) by ONE process through "
+    n = len(devs)
+    per_peer = 2 * k * k * 512 // (n * n)  # (k/N rows) x (2k/N columns) x 512 B
+    return {"workload": f"config 3: one k={k} square row-sharded over {n} GPU(s) by ONE process through "
                         "the C ABI (cel_shard_plan_*: in-library RCCL all-to-all + all-gather)",
-            "driver": "library", "transport": transport, "devices": devs,
+            "driver": "library", "transport": transport, "transport_note": note or None, "devices": devs,
+            "a2a_us": a2a_us, "a2a_bytes_per_peer": per_peer if a2a_us else 0,
+            "a2a_gbps_per_peer": per_peer / (a2a_us * 1e-6) / 1e9 if a2a_us else None,
+            "a2a_survey_estimate_us": per_peer / (XGMI_LINK_GBS * 1e9) * 1e6 if a2a_us else None,
             "value": steps / t1, "unit": "squares/s", "latency_ms": t1 / steps * 1e3, "steps": steps,
             "scaling": "strong",
             "pipelined": {"squares_in_flight": len(plans), "value": len(plans) * steps / tp, "unit": "squares/s",

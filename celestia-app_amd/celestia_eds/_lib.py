@@ -19,6 +19,7 @@ FLAG_ORDER_CHECK = 0x1
 FLAG_PARITY_ONLY = 0x2
 FLAG_CALLER_STREAM = 0x4
 FLAG_SHARD_EXCHANGE = 0x8
+FLAG_SHARD_PEERCOPY = 0x10
 SHARE_SIZE = 512
 NAMESPACE_SIZE = 29
 NMT_NODE_SIZE = 90
@@ -34,7 +35,7 @@ EXPORTS = [
     "cel_axis_trees", "cel_axis_tree", "cel_dah_tree", "cel_nmt_prove_range", "cel_merkle_aunts", "cel_commitment_paths",
     "cel_get_commitment", "cel_subtree_root_coordinates",
     "cel_extend_sharded", "cel_shard_plan_create", "cel_shard_plan_destroy", "cel_shard_plan_transport",
-    "cel_shard_plan_last_error", "cel_shard_plan_upload", "cel_shard_plan_run", "cel_shard_plan_wait",
+    "cel_shard_plan_last_error", "cel_shard_plan_note", "cel_shard_plan_time_exchange", "cel_shard_plan_upload", "cel_shard_plan_run", "cel_shard_plan_wait",
     "cel_extend_batch_multi", "cel_probe_sha256", "cel_probe_hbm_copy",
     "cel_probe_rs_transform",
 ]
@@ -109,6 +110,8 @@ def load():
             "cel_shard_plan_destroy": (None, [P]),
             "cel_shard_plan_transport": (ctypes.c_char_p, [P]),
             "cel_shard_plan_last_error": (ctypes.c_char_p, [P]),
+            "cel_shard_plan_note": (ctypes.c_char_p, [P]),
+            "cel_shard_plan_time_exchange": (i32, [P, u32, ctypes.POINTER(ctypes.c_double)]),
             "cel_shard_plan_upload": (i32, [P, P]),
             "cel_shard_plan_run": (i32, [P]),
             "cel_shard_plan_wait": (i32, [P, P, P, P, P]),

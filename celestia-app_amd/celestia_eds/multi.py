@@ -49,6 +49,19 @@ class ShardPlan:
     def transport(self):
         return self.lib.cel_shard_plan_transport(self.handle).decode()
 
+    @property
+    def note(self):
+        """Why RCCL was not used ("" when it was, or was not asked for)."""
+        return self.lib.cel_shard_plan_note(self.handle).decode()
+
+    def time_exchange(self, reps=10):
+        """Microseconds per all-to-all alone (slowest rank), or None for a one-rank plan in place."""
+        if self.transport == "local":
+            return None
+        us = ctypes.c_double()
+        self.check(self.lib.cel_shard_plan_time_exchange(self.handle, reps, ctypes.byref(us)))
+        return us.value
+
     def check(self, st):
         if st != _lib.OK:
             raise _lib.CelError(st, self.lib.cel_shard_plan_last_error(self.handle).decode()

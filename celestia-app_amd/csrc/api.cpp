@@ -67,6 +67,7 @@ cel_status cel_ctx_create(int device, cel_ctx** out) {
 
 void cel_ctx_destroy(cel_ctx* ctx) {
   if (!ctx) return;
+  destroy_ctx_worker(ctx);
   cel_shard_plan_destroy(ctx->shard_cache);
   {
     DeviceGuard g(ctx->device);

@@ -17,17 +17,24 @@
 // thread inside ncclGroupStart / ncclGroupEnd, NCCL's single-process multi-device pattern.
 // RCCL refuses two ranks on one device ("Duplicate GPU detected", profiles/r3_rccl_probe.txt);
 // a plan whose ctxs repeat a device therefore moves the same blocks with device copies
-// (transport "copy", hipMemcpyPeerAsync) in the same schedule, which is how the plan's N > 1
-// schedule is tested on a one-GPU box. Distinct devices always use RCCL. One rank needs no
-// collective (transport "local": the all-to-all is the identity, the row pass writes the slab
-// in place, and the gather is the rank's own record block) unless CEL_FLAG_SHARD_EXCHANGE asks
-// for the exchange through a one-rank RCCL communicator.
+// (transport "copy") in the same schedule, which is how the plan's N > 1 schedule is tested
+// on a one-GPU box. Distinct devices use RCCL, or hipMemcpyPeerAsync with peer access
+// enabled (transport "peer") when CEL_FLAG_SHARD_PEERCOPY asks for it or when RCCL cannot
+// start (not loadable, ncclCommInitAll failing): the plan then reports "peer-fallback" and
+// keeps RCCL's message in cel_shard_plan_note, so a node's first multi-GPU run cannot come
+// back empty-handed. One rank needs no collective (transport "local": the all-to-all is the
+// identity, the row pass writes the slab in place, and the gather is the rank's own record
+// block) unless CEL_FLAG_SHARD_EXCHANGE asks for the exchange through a one-rank RCCL
+// communicator. The selection is shard_transport.hpp's (unit-tested on the host).
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -36,6 +43,7 @@
 
 #include "api_common.hpp"
 #include "cel_internal.hpp"
+#include "shard_transport.hpp"
 
 using namespace cel;
 using namespace cel::abi;
@@ -90,7 +98,9 @@ const Rccl& rccl() {
 
 // One row-sharded square over ngpu devices: per-rank buffers, streams and communicators.
 struct cel_shard_plan {
-  enum Transport { kRccl, kCopy, kLocal };
+  using Transport = ShardTransport;
+  static constexpr Transport kRccl = Transport::kRccl, kCopy = Transport::kCopy, kLocal = Transport::kLocal,
+                             kPeer = Transport::kPeer;
   struct Rank {
     int device = 0;
     hipStream_t s = nullptr;
@@ -108,6 +118,8 @@ struct cel_shard_plan {
   uint32_t ngpu = 0, k = 0, w = 0, flags = 0;
   bool alias = false, ran = false;
   Transport transport = kRccl;
+  bool fallback = false;  // RCCL could not start: copies instead (note says why)
+  std::string note;
   std::vector<Rank> r;
   std::vector<ncclComm_t> comms;
   hipEvent_t ev_fin = nullptr;  // on rank 0's stream: the gather copies and the finish
@@ -158,6 +170,53 @@ void plan_free(cel_shard_plan* p) {
   if (p->host_out) (void)hipHostFree(p->host_out);
 }
 
+// A ctx's host worker for cel_extend_batch_multi: one thread running posted jobs in order.
+// Members before the thread, so the thread starts on constructed state.
+struct CtxWorker {
+  std::mutex m;
+  std::condition_variable cv;
+  std::deque<std::function<void()>> q;
+  bool stop = false;
+  std::thread th;
+  CtxWorker() : th([this] { loop(); }) {}
+  ~CtxWorker() {
+    {
+      std::lock_guard<std::mutex> l(m);
+      stop = true;
+    }
+    cv.notify_one();
+    th.join();
+  }
+  void post(std::function<void()> f) {
+    {
+      std::lock_guard<std::mutex> l(m);
+      q.push_back(std::move(f));
+    }
+    cv.notify_one();
+  }
+  void loop() {
+    for (;;) {
+      std::function<void()> f;
+      {
+        std::unique_lock<std::mutex> l(m);
+        cv.wait(l, [&] { return stop || !q.empty(); });
+        if (q.empty()) return;  // stop, queue drained
+        f = std::move(q.front());
+        q.pop_front();
+      }
+      f();
+    }
+  }
+};
+
+std::mutex g_worker_mu;  // creation of the ctxs' workers
+
+CtxWorker* ctx_worker(cel_ctx* c) {
+  std::lock_guard<std::mutex> l(g_worker_mu);
+  if (!c->worker) c->worker = new CtxWorker();
+  return static_cast<CtxWorker*>(c->worker);
+}
+
 // Device copy of `bytes` from (src_dev, src) to (dst_dev, dst) on stream s (of dst_dev).
 hipError_t dcopy(void* dst, int dst_dev, const void* src, int src_dev, size_t bytes, hipStream_t s) {
   if (dst_dev == src_dev) return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s);
@@ -165,6 +224,14 @@ hipError_t dcopy(void* dst, int dst_dev, const void* src, int src_dev, size_t by
 }
 
 }  // namespace
+
+namespace cel {
+void destroy_ctx_worker(cel_ctx* c) {
+  std::lock_guard<std::mutex> l(g_worker_mu);
+  delete static_cast<CtxWorker*>(c->worker);  // joins after the queued jobs
+  c->worker = nullptr;
+}
+}  // namespace cel
 
 extern "C" {
 
@@ -185,15 +252,13 @@ cel_status cel_shard_plan_create(cel_ctx* const* ctxs, uint32_t ngpu, uint32_t k
   p->k = k;
   p->w = 2 * k / ngpu;
   p->flags = flags;
-  p->alias = ngpu == 1 && !(flags & CEL_FLAG_SHARD_EXCHANGE);  // one rank, no collective
   p->r.resize(ngpu);
   std::vector<int> devs(ngpu);
   for (uint32_t i = 0; i < ngpu; i++) devs[i] = p->r[i].device = ctxs[i]->device;
-  std::vector<int> sorted = devs;
-  std::sort(sorted.begin(), sorted.end());
-  p->transport = p->alias ? cel_shard_plan::kLocal
-                 : std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end() ? cel_shard_plan::kRccl
-                                                                                    : cel_shard_plan::kCopy;
+  const ShardChoice choice = shard_choose(devs.data(), ngpu, (flags & CEL_FLAG_SHARD_EXCHANGE) != 0,
+                                          (flags & CEL_FLAG_SHARD_PEERCOPY) != 0);
+  p->alias = choice.alias;  // one rank, no collective
+  p->transport = choice.want;
   auto bail = [&](cel_status st, const std::string& msg) {
     c0->last_error = msg;
     plan_free(p);
@@ -236,13 +301,35 @@ cel_status cel_shard_plan_create(cel_ctx* const* ctxs, uint32_t ngpu, uint32_t k
     return bail(CEL_ENOMEM, "shard plan: page-locked host buffer");
   if (p->transport == cel_shard_plan::kRccl) {
     const Rccl& nc = rccl();
-    if (!nc.error.empty()) return bail(CEL_EDEVICE, nc.error);
-    p->comms.assign(ngpu, nullptr);
-    const ncclResult_t r = nc.CommInitAll(p->comms.data(), (int)ngpu, devs.data());
-    if (r != ncclSuccess) {
+    bool ok = nc.error.empty();
+    if (!ok) {
+      p->note = nc.error;
+    } else {
       p->comms.assign(ngpu, nullptr);
-      return bail(CEL_EDEVICE, std::string("ncclCommInitAll: ") + nc.GetErrorString(r));
+      const ncclResult_t r = nc.CommInitAll(p->comms.data(), (int)ngpu, devs.data());
+      ok = r == ncclSuccess;
+      if (!ok) {
+        p->comms.clear();
+        p->note = std::string("ncclCommInitAll: ") + nc.GetErrorString(r);
+      }
     }
+    p->transport = shard_settle(choice, ok);
+    p->fallback = !ok;
+  }
+  if (p->transport == cel_shard_plan::kPeer) {
+    // direct reads of the peers' buffers where the link allows it; hipMemcpyPeerAsync works
+    // either way (staged by the runtime when it does not)
+    for (uint32_t i = 0; i < ngpu; i++)
+      for (uint32_t j = 0; j < ngpu; j++) {
+        int can = 0;
+        if (i == j || hipDeviceCanAccessPeer(&can, devs[i], devs[j]) != hipSuccess || !can) continue;
+        DeviceGuard g(devs[i]);
+        const hipError_t e = hipDeviceEnablePeerAccess(devs[j], 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+          return bail(CEL_EDEVICE, std::string("shard plan: peer access ") + std::to_string(devs[i]) + " -> " +
+                                       std::to_string(devs[j]) + ": " + hipGetErrorString(e));
+        (void)hipGetLastError();
+      }
   }
   *out = p;
   return CEL_OK;
@@ -255,9 +342,10 @@ void cel_shard_plan_destroy(cel_shard_plan* plan) {
 }
 
 const char* cel_shard_plan_transport(const cel_shard_plan* plan) {
-  if (!plan) return "";
-  return plan->transport == cel_shard_plan::kRccl ? "rccl" : plan->transport == cel_shard_plan::kCopy ? "copy" : "local";
+  return plan ? shard_transport_name(plan->transport, plan->fallback) : "";
 }
+
+const char* cel_shard_plan_note(const cel_shard_plan* plan) { return plan ? plan->note.c_str() : ""; }
 
 const char* cel_shard_plan_last_error(const cel_shard_plan* plan) { return plan ? plan->last_error.c_str() : ""; }
 
@@ -275,6 +363,38 @@ cel_status cel_shard_plan_upload(cel_shard_plan* p, const uint8_t* ods) {
   return CEL_OK;
 }
 
+// The all-to-all of one run on the ranks' streams: rank h receives block h of every rank r
+// into its slab rows [r k/N, (r+1) k/N). Copy / peer transports wait for every rank's row pass
+// (ev_rows) and record ev_exch; RCCL orders it on the streams itself.
+static cel_status exchange(cel_shard_plan* p) {
+  const uint32_t N = p->ngpu;
+  const uint64_t blk = p->block_bytes();
+  hipError_t e = hipSuccess;
+  if (p->transport == cel_shard_plan::kCopy || p->transport == cel_shard_plan::kPeer) {
+    for (uint32_t h = 0; h < N && e == hipSuccess; h++) {
+      auto& dst = p->r[h];
+      DeviceGuard g(dst.device);
+      for (uint32_t r = 0; r < N && e == hipSuccess; r++) e = hipStreamWaitEvent(dst.s, p->r[r].ev_rows, 0);
+      for (uint32_t r = 0; r < N && e == hipSuccess; r++)
+        e = dcopy(dst.slab + r * blk, dst.device, p->r[r].send + h * blk, p->r[r].device, blk, dst.s);
+      if (e == hipSuccess) e = hipEventRecord(dst.ev_exch, dst.s);
+    }
+    return e == hipSuccess ? CEL_OK : plan_hip(p, e, "shard exchange");
+  }
+  const Rccl& nc = rccl();
+  ncclResult_t rc = nc.GroupStart();
+  for (uint32_t r = 0; r < N && rc == ncclSuccess; r++) {
+    auto& rk = p->r[r];
+    for (uint32_t h = 0; h < N && rc == ncclSuccess; h++) {
+      rc = nc.Send(rk.send + h * blk, blk, ncclUint8, (int)h, p->comms[r], rk.s);
+      if (rc == ncclSuccess) rc = nc.Recv(rk.slab + h * blk, blk, ncclUint8, (int)h, p->comms[r], rk.s);
+    }
+  }
+  const ncclResult_t rc2 = nc.GroupEnd();
+  if (rc != ncclSuccess || rc2 != ncclSuccess) return plan_nccl(p, rc != ncclSuccess ? rc : rc2, "all-to-all");
+  return CEL_OK;
+}
+
 // One square through the plan, asynchronous on the ranks' streams:
 //   rows (each rank) -> all-to-all of the column blocks -> cols + slab commit (each rank)
 //   -> all-gather of the record blocks -> finish (rank 0: row-root combine + DAH).
@@ -283,9 +403,8 @@ cel_status cel_shard_plan_run(cel_shard_plan* p) {
   std::lock_guard<std::mutex> lock(p->mu);
   const uint32_t N = p->ngpu, k = p->k;
   const bool order = (p->flags & CEL_FLAG_ORDER_CHECK) != 0;
-  const uint64_t blk = p->block_bytes();
   const size_t pb = p->pack_bytes();
-  const bool copy = p->transport == cel_shard_plan::kCopy;
+  const bool copy = p->transport == cel_shard_plan::kCopy || p->transport == cel_shard_plan::kPeer;
   hipError_t e = hipSuccess;
   // 1. rows. With copy transport, a rank's send buffer and record block are read by other
   //    ranks' streams: wait for the previous run's exchange and gather first.
@@ -302,29 +421,8 @@ cel_status cel_shard_plan_run(cel_shard_plan* p) {
   }
   // 2. all-to-all: rank h receives block h of every rank r into slab rows [r k/N, (r+1) k/N)
   if (!p->alias) {
-    if (copy) {
-      for (uint32_t h = 0; h < N && e == hipSuccess; h++) {
-        auto& dst = p->r[h];
-        DeviceGuard g(dst.device);
-        for (uint32_t r = 0; r < N && e == hipSuccess; r++) e = hipStreamWaitEvent(dst.s, p->r[r].ev_rows, 0);
-        for (uint32_t r = 0; r < N && e == hipSuccess; r++)
-          e = dcopy(dst.slab + r * blk, dst.device, p->r[r].send + h * blk, p->r[r].device, blk, dst.s);
-        if (e == hipSuccess) e = hipEventRecord(dst.ev_exch, dst.s);
-      }
-      if (e != hipSuccess) return plan_hip(p, e, "shard exchange");
-    } else {
-      const Rccl& nc = rccl();
-      ncclResult_t rc = nc.GroupStart();
-      for (uint32_t r = 0; r < N && rc == ncclSuccess; r++) {
-        auto& rk = p->r[r];
-        for (uint32_t h = 0; h < N && rc == ncclSuccess; h++) {
-          rc = nc.Send(rk.send + h * blk, blk, ncclUint8, (int)h, p->comms[r], rk.s);
-          if (rc == ncclSuccess) rc = nc.Recv(rk.slab + h * blk, blk, ncclUint8, (int)h, p->comms[r], rk.s);
-        }
-      }
-      const ncclResult_t rc2 = nc.GroupEnd();
-      if (rc != ncclSuccess || rc2 != ncclSuccess) return plan_nccl(p, rc != ncclSuccess ? rc : rc2, "all-to-all");
-    }
+    const cel_status xs = exchange(p);
+    if (xs) return xs;
   }
   // 3. cols + slab commit: the record block is [row subtrees 2k | column roots w | status]
   for (uint32_t i = 0; i < N; i++) {
@@ -418,6 +516,53 @@ cel_status cel_shard_plan_wait(cel_shard_plan* p, uint8_t* eds_out, uint8_t* row
   return st ? plan_fail(p, st, "shard plan: device status " + std::to_string(st)) : CEL_OK;
 }
 
+// The all-to-all alone (bench.py's rowshard512_lib): one exchange to warm up, then `reps`
+// back to back on every rank's stream, bracketed by timing events per rank after the queued
+// runs drain; the longest rank's average. The send buffers and slabs hold whatever the last
+// run left (the bytes moved are the same).
+cel_status cel_shard_plan_time_exchange(cel_shard_plan* p, uint32_t reps, double* us_per_exchange) {
+  if (!p || !us_per_exchange || !reps) return CEL_EINVAL;
+  std::lock_guard<std::mutex> lock(p->mu);
+  if (p->alias) return plan_fail(p, CEL_EINVAL, "shard plan: one rank in place, no exchange to time");
+  const uint32_t N = p->ngpu;
+  std::vector<hipEvent_t> a(N, nullptr), b(N, nullptr);
+  hipError_t e = hipSuccess;
+  cel_status st = CEL_OK;
+  for (uint32_t i = 0; i < N && e == hipSuccess; i++) {
+    DeviceGuard g(p->r[i].device);
+    e = hipStreamSynchronize(p->r[i].s);
+    if (e == hipSuccess) e = hipEventCreate(&a[i]);
+    if (e == hipSuccess) e = hipEventCreate(&b[i]);
+    if (e == hipSuccess) e = hipEventRecord(p->r[i].ev_rows, p->r[i].s);  // the copies' wait: satisfied
+  }
+  for (uint32_t it = 0; it <= reps && e == hipSuccess && !st; it++) {
+    if (it == 1)
+      for (uint32_t i = 0; i < N && e == hipSuccess; i++) {
+        DeviceGuard g(p->r[i].device);
+        e = hipEventRecord(a[i], p->r[i].s);
+      }
+    if (e == hipSuccess) st = exchange(p);
+  }
+  double worst = 0;
+  for (uint32_t i = 0; i < N && e == hipSuccess && !st; i++) {
+    DeviceGuard g(p->r[i].device);
+    e = hipEventRecord(b[i], p->r[i].s);
+    if (e == hipSuccess) e = hipEventSynchronize(b[i]);
+    float ms = 0;
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, a[i], b[i]);
+    worst = std::max(worst, (double)ms);
+  }
+  for (uint32_t i = 0; i < N; i++) {
+    DeviceGuard g(p->r[i].device);
+    if (a[i]) (void)hipEventDestroy(a[i]);
+    if (b[i]) (void)hipEventDestroy(b[i]);
+  }
+  if (st) return st;
+  if (e != hipSuccess) return plan_hip(p, e, "shard exchange timing");
+  *us_per_exchange = worst * 1e3 / reps;
+  return CEL_OK;
+}
+
 // da.ExtendShares + NewDataAvailabilityHeader for one square over ngpu devices. The plan
 // (buffers, streams, communicators: ncclCommInitAll is the expensive part) is kept in
 // ctxs[0] and reused while the device list, k and flags stay the same.
@@ -448,8 +593,10 @@ cel_status cel_extend_sharded(cel_ctx* const* ctxs, uint32_t ngpu, const uint8_t
 }
 
 // Config 4 over several devices: squares [first_i, first_i + n_i) go to ctxs[i] (an equal
-// split, the remainder to the first ctxs), each through cel_extend_batch on its own host
-// thread (ctxs[0] on the caller's), so the ctxs' PCIe copies and kernels run side by side.
+// split, the remainder to the first ctxs), each through cel_extend_batch on that ctx's host
+// worker thread (ctxs[0]'s part on the caller's), so the ctxs' PCIe copies and kernels run
+// side by side. The workers live as long as their ctx: a call posts its parts and waits on
+// a per-call latch, no thread is started per call.
 cel_status cel_extend_batch_multi(cel_ctx* const* ctxs, uint32_t ngpu, const uint8_t* ods, uint32_t n, uint32_t k,
                                   uint32_t share_size, uint8_t* eds_out, uint8_t* row_roots, uint8_t* col_roots,
                                   uint8_t* dah, int32_t* status_out, uint32_t flags) {
@@ -466,20 +613,44 @@ cel_status cel_extend_batch_multi(cel_ctx* const* ctxs, uint32_t ngpu, const uin
     f += cnt[i];
   }
   auto part = [&](uint32_t i) {
-    if (!cnt[i]) return;
     const uint64_t f = first[i];
     st[i] = cel_extend_batch(ctxs[i], ods + f * ods_sq, cnt[i], k, share_size, eds_out ? eds_out + f * eds_sq : nullptr,
                              row_roots + f * roots_sq, col_roots + f * roots_sq, dah + f * 32,
                              status_out ? status_out + f : nullptr, flags);
   };
-  std::vector<std::thread> th;
-  for (uint32_t i = 1; i < ngpu; i++) th.emplace_back(part, i);
-  part(0);
-  for (auto& t : th) t.join();
-  // the first failing part's status; its message to ctxs[0] (order failures are per square)
+  std::mutex m;
+  std::condition_variable cv;
+  uint32_t pending = 0;
+  for (uint32_t i = 1; i < ngpu; i++) {
+    if (!cnt[i]) continue;
+    {
+      std::lock_guard<std::mutex> l(m);
+      pending++;
+    }
+    ctx_worker(ctxs[i])->post([&, i] {
+      part(i);
+      std::lock_guard<std::mutex> l(m);
+      if (--pending == 0) cv.notify_one();
+    });
+  }
+  if (cnt[0]) part(0);
+  {
+    std::unique_lock<std::mutex> l(m);
+    cv.wait(l, [&] { return pending == 0; });
+  }
+  // the first failing part's status; its message to ctxs[0] (order failures are per square),
+  // read and written under each ctx's lock
   for (uint32_t i = 0; i < ngpu; i++)
     if (st[i] != CEL_OK) {
-      if (i) ctxs[0]->last_error = cel_last_error(ctxs[i]);
+      if (ctxs[i] != ctxs[0]) {
+        std::string msg;
+        {
+          std::lock_guard<std::mutex> l(ctxs[i]->mu);
+          msg = ctxs[i]->last_error;
+        }
+        std::lock_guard<std::mutex> l(ctxs[0]->mu);
+        ctxs[0]->last_error = msg;
+      }
       return st[i];
     }
   return CEL_OK;

@@ -266,4 +266,10 @@ struct cel_ctx {
   // cel_extend_sharded's plan (buffers, streams, RCCL communicators), kept while the device
   // list, k and flags stay the same (api_multi.cpp)
   cel_shard_plan* shard_cache = nullptr;
+  // cel_extend_batch_multi's host worker thread for this ctx (api_multi.cpp), made on first use
+  void* worker = nullptr;
 };
+
+namespace cel {
+void destroy_ctx_worker(cel_ctx* c);  // api_multi.cpp: joins the ctx's worker, if any
+}

@@ -183,7 +183,10 @@ cel_status cel_dev_shard_finish(cel_ctx* ctx, const void* d_gathered, uint32_t k
  * ncclGroupStart / ncclGroupEnd. librccl.so.1 is loaded (dlopen) by the first plan over
  * distinct devices; the single-device entry points never need it. RCCL refuses two ranks on
  * one device, so a plan whose ctxs repeat a device moves the same blocks with device copies
- * instead (transport "copy": the same schedule, e.g. N ranks rehearsed on one GPU).
+ * instead (transport "copy": the same schedule, e.g. N ranks rehearsed on one GPU). Distinct
+ * devices without RCCL (CEL_FLAG_SHARD_PEERCOPY, or RCCL not loadable / ncclCommInitAll
+ * failing at plan creation) move them with hipMemcpyPeerAsync, peer access enabled (transport
+ * "peer", "peer-fallback" when RCCL failed; cel_shard_plan_note keeps RCCL's message).
  *
  * cel_extend_sharded: da.ExtendShares + da.NewDataAvailabilityHeader
  * (data_availability_header.go:65-75, :44-63) for ONE square row-sharded over ngpu devices
@@ -205,23 +208,39 @@ cel_status cel_extend_sharded(cel_ctx* const* ctxs, uint32_t ngpu, const uint8_t
  *   run      one square, asynchronous on the ranks' streams;
  *   wait     sync, then (each nullable) the EDS (from every rank's column slab), the roots and
  *            the DAH (rank 0); returns the square's status (CEL_EORDER) or a device error.
- * flags: CEL_FLAG_ORDER_CHECK, CEL_FLAG_PARITY_ONLY (wait's eds_out), CEL_FLAG_SHARD_EXCHANGE. */
+ * flags: CEL_FLAG_ORDER_CHECK, CEL_FLAG_PARITY_ONLY (wait's eds_out), CEL_FLAG_SHARD_EXCHANGE,
+ * CEL_FLAG_SHARD_PEERCOPY. */
 typedef struct cel_shard_plan cel_shard_plan;
-#define CEL_FLAG_SHARD_EXCHANGE 0x8u /* ngpu = 1: a one-rank RCCL communicator, a separate send buffer,
-                                        the all-to-all through it (self send / receive) and the record
+#define CEL_FLAG_SHARD_EXCHANGE 0x8u /* the exchange through RCCL wherever it is asked for: ngpu = 1
+                                        gets a one-rank RCCL communicator, a separate send buffer, the
+                                        all-to-all through it (self send / receive) and the record
                                         all-gather too, instead of the row pass writing the slab in
-                                        place and no collective (tests the N > 1 exchange on one GPU) */
+                                        place and no collective (tests the N > 1 exchange on one GPU);
+                                        ctxs repeating a device try RCCL too (which refuses them) and
+                                        fall back to device copies ("copy-fallback") */
+#define CEL_FLAG_SHARD_PEERCOPY 0x10u /* never RCCL: distinct devices exchange with hipMemcpyPeerAsync
+                                         (transport "peer"), repeated devices with device copies */
 cel_status cel_shard_plan_create(cel_ctx* const* ctxs, uint32_t ngpu, uint32_t k, uint32_t flags,
                                  cel_shard_plan** out);
 void cel_shard_plan_destroy(cel_shard_plan* plan);
 const char* cel_shard_plan_transport(const cel_shard_plan* plan); /* "rccl", "copy" (ctxs repeat a
-                                                                      device) or "local" (one rank,
-                                                                      no collective) */
+                                                                      device), "peer" (distinct
+                                                                      devices, peer copies), "local"
+                                                                      (one rank, no collective);
+                                                                      "copy-fallback" /
+                                                                      "peer-fallback" when RCCL
+                                                                      could not start */
+const char* cel_shard_plan_note(const cel_shard_plan* plan); /* why RCCL was not used ("" if it was,
+                                                               or was not asked for) */
 const char* cel_shard_plan_last_error(const cel_shard_plan* plan);
 cel_status cel_shard_plan_upload(cel_shard_plan* plan, const uint8_t* ods);
 cel_status cel_shard_plan_run(cel_shard_plan* plan);
 cel_status cel_shard_plan_wait(cel_shard_plan* plan, uint8_t* eds_out, uint8_t* row_roots, uint8_t* col_roots,
                                uint8_t* dah);
+/* The plan's all-to-all alone, `reps` times back to back after one warm-up exchange: the
+ * slowest rank's microseconds per exchange (a report's figure next to SURVEY.md §8e's
+ * one-link estimate; CEL_EINVAL for a one-rank plan in place, which has no exchange). */
+cel_status cel_shard_plan_time_exchange(cel_shard_plan* plan, uint32_t reps, double* us_per_exchange);
 /* Config 4 over several devices: cel_extend_batch's arguments, the n squares split into ngpu
  * contiguous ranges (sizes differ by at most one) each extended by cel_extend_batch on ctxs[i]
  * from its own host thread, so every device's PCIe copies and kernels run side by side

@@ -94,6 +94,43 @@ def test_shard_plan_copy_transport(ctxs, oracle, k, n):
     plan.close()
 
 
+def test_shard_plan_rccl_refused_falls_back(ctxs, oracle):
+    """RCCL that cannot start leaves the plan on device copies instead of failing: two ranks
+    on the box's one device with CEL_FLAG_SHARD_EXCHANGE make ncclCommInitAll refuse them
+    (duplicate GPU, profiles/r3_rccl_probe.txt), the plan reports "copy-fallback" with RCCL's
+    message, and the square is bit-exact (the path distinct devices take as "peer-fallback")."""
+    from celestia_eds import _lib
+    from celestia_eds.multi import ShardPlan
+    k = 256
+    plan = ShardPlan(ctxs[:2], k, _lib.FLAG_ORDER_CHECK | _lib.FLAG_SHARD_EXCHANGE)
+    assert plan.transport == "copy-fallback", plan.transport
+    assert "ncclCommInitAll" in plan.note or "RCCL" in plan.note, plan.note
+    plan.upload(random_ods(k, 925))
+    plan.run()
+    assert_square(plan.wait(want_eds=True), expected(oracle, k, 925))
+    assert plan.time_exchange(3) > 0
+    plan.close()
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_shard_plan_peercopy_flag(ctxs, oracle, n):
+    """CEL_FLAG_SHARD_PEERCOPY never starts RCCL: repeated devices take the copy transport
+    (distinct devices would take "peer"), no note, bit-exact; the exchange times alone."""
+    from celestia_eds import _lib
+    from celestia_eds.multi import ShardPlan
+    k = 256
+    plan = ShardPlan(ctxs[:n], k, _lib.FLAG_ORDER_CHECK | _lib.FLAG_SHARD_PEERCOPY)
+    assert plan.transport == "copy" and plan.note == ""
+    plan.upload(random_ods(k, 926))
+    plan.run()
+    assert_square(plan.wait(want_eds=True), expected(oracle, k, 926))
+    assert plan.time_exchange(3) > 0
+    plan.close()
+    local = ShardPlan(ctxs[:1], k, _lib.FLAG_ORDER_CHECK | _lib.FLAG_SHARD_PEERCOPY)
+    assert local.transport == "local" and local.time_exchange() is None
+    local.close()
+
+
 def test_shard_plans_in_flight(ctxs, oracle):
     """Two plans (own streams and communicators) with squares in flight at once."""
     from celestia_eds.multi import ShardPlan
