@@ -75,7 +75,11 @@ def _rs_traffic(k, batch, layout):
         return None
     if p.get("k") != k:
         return None
+    sq = p["squares"]
+    read = 2 * sum(p["fetch_kib_raw"].values()) * 1024 / sq  # FETCH_SIZE doubled (gfx950)
+    write = sum(p["write_kib"].values()) * 1024 / sq
     return {"bytes": p["bytes_per_square"] * batch, "per_square": p["bytes_per_square"],
+            "read_per_square": read, "write_per_square": write,
             "vs_algorithmic": p["bytes_per_square"] / p["algorithmic_bytes_per_square"],
             "source": f"profiles/{name} (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, KiB)"}
 
@@ -1239,9 +1243,23 @@ def main():
         # same-run denominators (cel_probe_*, before the timed region, this rank's device)
         result["probe"] = {**probe, "basis": "cel_probe_sha256 (NMT compression chained in registers, 16 WG/CU; "
                                              "shader clock = s_memtime ticks per s_memrealtime tick over that "
-                                             "launch) and cel_probe_hbm_copy (4 GiB streaming copy, read + write)"}
+                                             "launch) and cel_probe_hbm_stream (4 GiB: float4 streaming copy, read + write; "
+                                             "read-only and write-only streams)"}
         result["roofline"]["achievable"] = probe["hbm_copy_gbps"]
+        result["roofline"]["achievable_basis"] = "cel_probe_hbm_copy: float4 streaming copy, one element per lane"
         result["roofline"]["frac_of_achievable_hbm"] = rs_gbs / probe["hbm_copy_gbps"]
+        tr = result["roofline"]["traffic"]
+        if tr and probe.get("hbm_read_gbps") and probe.get("hbm_write_gbps"):
+            # the extension's own mix: its measured read and write bytes at this box's read-only
+            # and write-only stream rates (HBM writes stream ~30 % slower than reads)
+            t_sq = tr["read_per_square"] / (probe["hbm_read_gbps"] * 1e9) + \
+                tr["write_per_square"] / (probe["hbm_write_gbps"] * 1e9)
+            mix = 2048 * k * k / t_sq / 1e9
+            result["roofline"]["achievable_mix"] = mix
+            result["roofline"]["frac_of_achievable_mix"] = rs_gbs / mix
+            result["roofline"]["achievable_mix_basis"] = ("algorithmic bytes over the time the measured traffic "
+                                                          "(read_per_square, write_per_square) takes at the "
+                                                          "probe's read-only and write-only rates")
         result["roofline_nmt"]["peak_same_run"] = probe["sha256_gcomp_per_s"]
         result["roofline_nmt"]["frac_same_run"] = nmt_rate / 1e9 / probe["sha256_gcomp_per_s"]
         result["shader_mhz"] = probe["shader_mhz"]

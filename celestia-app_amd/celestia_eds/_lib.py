@@ -36,7 +36,7 @@ EXPORTS = [
     "cel_get_commitment", "cel_subtree_root_coordinates",
     "cel_extend_sharded", "cel_shard_plan_create", "cel_shard_plan_destroy", "cel_shard_plan_transport",
     "cel_shard_plan_last_error", "cel_shard_plan_note", "cel_shard_plan_time_exchange", "cel_shard_plan_upload", "cel_shard_plan_run", "cel_shard_plan_wait",
-    "cel_extend_batch_multi", "cel_probe_sha256", "cel_probe_hbm_copy",
+    "cel_extend_batch_multi", "cel_probe_sha256", "cel_probe_hbm_copy", "cel_probe_hbm_stream",
     "cel_probe_rs_transform",
 ]
 
@@ -118,6 +118,7 @@ def load():
             "cel_extend_batch_multi": (i32, [P, u32, P, u32, u32, u32, P, P, P, P, P, u32]),
             "cel_probe_sha256": (i32, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
             "cel_probe_hbm_copy": (i32, [P, u64, ctypes.POINTER(ctypes.c_double)]),
+            "cel_probe_hbm_stream": (i32, [P, u64] + [ctypes.POINTER(ctypes.c_double)] * 3),
             "cel_probe_rs_transform": (i32, [P, u32, ctypes.POINTER(ctypes.c_double)]),
         }
         for name, (res, args) in sigs.items():

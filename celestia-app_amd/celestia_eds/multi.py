@@ -134,13 +134,15 @@ def extend_batch_multi(ctxs, ods, want_eds=True, flags=_lib.FLAG_ORDER_CHECK):
 
 def probe(ctx, hbm_bytes=4 << 30, rs_k=(64, 128, 512)):
     """Same-run ceilings on ctx's device: SHA-256 G compressions/s in registers, the
-    sustained shader clock over that launch (MHz), streaming-copy HBM GB/s, and the
+    sustained shader clock over that launch (MHz), streaming-copy HBM GB/s (and the
+    read-only / write-only stream rates), and the
     microseconds of VALU one k-square's extension takes with no HBM traffic
     (`rs_transform_us_k<k>`, each k in rs_k; GF(2^8) up to k = 128, GF(2^16) at 256 / 512)."""
-    g, mhz, bw = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+    g, mhz, bw, rd, wr = (ctypes.c_double() for _ in range(5))
     ctx.check(ctx.lib.cel_probe_sha256(ctx.handle, ctypes.byref(g), ctypes.byref(mhz)))
-    ctx.check(ctx.lib.cel_probe_hbm_copy(ctx.handle, hbm_bytes, ctypes.byref(bw)))
-    out = {"sha256_gcomp_per_s": g.value, "shader_mhz": mhz.value, "hbm_copy_gbps": bw.value}
+    ctx.check(ctx.lib.cel_probe_hbm_stream(ctx.handle, hbm_bytes, ctypes.byref(bw), ctypes.byref(rd), ctypes.byref(wr)))
+    out = {"sha256_gcomp_per_s": g.value, "shader_mhz": mhz.value, "hbm_copy_gbps": bw.value,
+           "hbm_read_gbps": rd.value, "hbm_write_gbps": wr.value}
     for k in rs_k:
         us = ctypes.c_double()
         ctx.check(ctx.lib.cel_probe_rs_transform(ctx.handle, k, ctypes.byref(us)))

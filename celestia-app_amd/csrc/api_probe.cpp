@@ -78,31 +78,47 @@ cel_status cel_probe_sha256(cel_ctx* ctx, double* g_compressions_per_s, double* 
 }
 
 cel_status cel_probe_hbm_copy(cel_ctx* ctx, uint64_t bytes, double* gbps) {
-  if (!ctx || !gbps || bytes < 2 * 16) return CEL_EINVAL;
+  return cel_probe_hbm_stream(ctx, bytes, gbps, nullptr, nullptr);
+}
+
+cel_status cel_probe_hbm_stream(cel_ctx* ctx, uint64_t bytes, double* copy_gbps, double* read_gbps,
+                                double* write_gbps) {
+  if (!ctx || !copy_gbps || bytes < 2 * 4096) return CEL_EINVAL;
   std::lock_guard<std::mutex> lock(ctx->mu);
   DeviceGuard g(ctx->device);
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess)
     return fail(ctx, CEL_EDEVICE, "device attributes");
-  const uint64_t half = (bytes / 2) & ~(uint64_t)4095;  // read half, write half
+  const uint64_t half = (bytes / 2) & ~(uint64_t)4095;  // copy: read half, write half
   void *src = nullptr, *dst = nullptr;
   hipError_t e = hipMalloc(&src, half);
   if (e == hipSuccess) e = hipMalloc(&dst, half);
   if (e == hipSuccess) e = hipMemsetAsync(src, 0x5A, half, ctx->stream);
-  // the fastest of {non-temporal, default policy} x {8, 16 workgroups per CU}
+  // copy: the faster of {non-temporal, default policy}
   double secs = 1e30;
-  for (int v = 0; v < 4 && e == hipSuccess; v++) {
+  for (int v = 0; v < 2 && e == hipSuccess; v++) {
     double t = 0;
-    const bool nt = v & 1;
-    const uint32_t blocks = (uint32_t)cus * (v < 2 ? 8 : 16);
-    e = best_time([&] { return launch_probe_copy(src, dst, half, blocks, nt, ctx->stream); }, 5, ctx->stream, &t);
+    e = best_time([&] { return launch_probe_copy(src, dst, half, 0, 0, v == 0, ctx->stream); }, 5, ctx->stream, &t);
     secs = std::min(secs, t);
+  }
+  // read-only and write-only streams over the same half: the fastest of 4 / 8 / 16 workgroups per CU
+  double rsecs = 1e30, wsecs = 1e30;
+  for (int v = 0; v < 6 && e == hipSuccess && (read_gbps || write_gbps); v++) {
+    const int mode = v < 3 ? 1 : 2;
+    if ((mode == 1 && !read_gbps) || (mode == 2 && !write_gbps)) continue;
+    const uint32_t blocks = (uint32_t)cus * (4u << (v % 3));
+    double t = 0;
+    e = best_time([&] { return launch_probe_copy(src, dst, half, blocks, mode, true, ctx->stream); }, 5, ctx->stream,
+                  &t);
+    (mode == 1 ? rsecs : wsecs) = std::min(mode == 1 ? rsecs : wsecs, t);
   }
   if (src) (void)hipFree(src);
   if (dst) (void)hipFree(dst);
   if (e != hipSuccess) return e == hipErrorOutOfMemory ? fail(ctx, CEL_ENOMEM, "device allocation failed")
                                                        : hip_fail(ctx, e, "hbm probe");
-  *gbps = 2.0 * (double)half / secs / 1e9;
+  *copy_gbps = 2.0 * (double)half / secs / 1e9;
+  if (read_gbps) *read_gbps = (double)half / rsecs / 1e9;
+  if (write_gbps) *write_gbps = (double)half / wsecs / 1e9;
   return CEL_OK;
 }
 

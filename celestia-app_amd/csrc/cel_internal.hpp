@@ -170,7 +170,10 @@ hipError_t launch_shard_finish(const uint32_t* gathered, uint32_t k, uint32_t nr
 // Same-run probes (probe_kernels.hip): SHA-256 chained in registers (out: blocks*256 words,
 // clk: 2 counters per wave), and a streaming copy of `bytes` (a multiple of 16).
 hipError_t launch_probe_sha(uint32_t* out, unsigned long long* clk, uint32_t blocks, int n, hipStream_t s);
-hipError_t launch_probe_copy(const void* src, void* dst, uint64_t bytes, uint32_t blocks, bool nt, hipStream_t s);
+// mode 0: copy `bytes` from src to dst (one lane per 16-byte element; blocks unused); 1: read
+// src only; 2: write dst only (grid-strided over `blocks` workgroups)
+hipError_t launch_probe_copy(const void* src, void* dst, uint64_t bytes, uint32_t blocks, int mode, bool nt,
+                             hipStream_t s);
 // GF(2^8) encode transform alone (rs_axis.hip), k = 32/64/128: ntiles tiles reading the same
 // k x 256 B of src; dst (k x 256 B) written only when store != 0.
 hipError_t launch_probe_rs_transform(uint32_t k, const uint32_t* src, uint32_t* dst, uint32_t ntiles, uint32_t store,

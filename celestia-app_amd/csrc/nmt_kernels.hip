@@ -395,11 +395,14 @@ __device__ __forceinline__ void sha_empty(uint32_t (&st)[8]) {
 // (a multiple of 16) from out_src (roots | dah | status, written before the copy) to host_out,
 // page-locked host memory, with 16-byte stores: the results cross PCIe inside this launch
 // instead of in a separate copy after it.
+// row_out, col_out, dah and status may all lie inside [out_src, out_src + out_bytes) (the
+// one-square path copies that block out to host_out after writing it), so none of the four
+// nor out_src is __restrict__: the copy-out loads must see thread 0's dah / status stores.
 __global__ __launch_bounds__(1024) void k_merkle(const uint32_t* __restrict__ items, const uint32_t* __restrict__ leafd,
-                                                uint32_t n, uint8_t* __restrict__ dah, uint8_t* __restrict__ row_out,
-                                                uint8_t* __restrict__ col_out, const int32_t* __restrict__ bad_axis,
-                                                int32_t* __restrict__ status, const uint8_t* __restrict__ out_src = nullptr,
-                                                uint8_t* __restrict__ host_out = nullptr, uint32_t out_bytes = 0) {
+                                                uint32_t n, uint8_t* dah, uint8_t* row_out, uint8_t* col_out,
+                                                const int32_t* __restrict__ bad_axis, int32_t* status,
+                                                const uint8_t* out_src = nullptr, uint8_t* __restrict__ host_out = nullptr,
+                                                uint32_t out_bytes = 0) {
   extern __shared__ __attribute__((aligned(16))) uint32_t hs[];  // n * 8 words
   const uint32_t g = blockIdx.x;
   const uint32_t* it = items + (uint64_t)g * n * kNodeWords;

@@ -7,9 +7,9 @@
 //                 the shader-clock counter (s_memtime) and the constant-rate counter
 //                 (s_memrealtime) at its start and end, so the sustained clock under a
 //                 VALU-bound load comes from the same launch.
-//   k_probe_copy  a streaming copy (16 KiB chunks per workgroup, four dwordx4 loads in
-//                 flight per lane, non-temporal or default policy): achievable HBM bytes/s,
-//                 read + write.
+//   k_probe_copy  a streaming copy (one 16-byte element per lane, non-temporal or default
+//                 policy): achievable HBM bytes/s, read + write; and the read-only and
+//                 write-only streams of the same elements.
 #include <hip/hip_runtime.h>
 
 #include "cel_internal.hpp"
@@ -44,30 +44,33 @@ __global__ __launch_bounds__(256, 4) void k_probe_sha(uint32_t* out, unsigned lo
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// Each workgroup copies contiguous 16 KiB chunks (four dwordx4 loads in flight per lane
-// before their stores), chunk index grid-strided: the fastest shape of the sweep in
-// tools/microbench/hbm_copy.hip (profiles/r5_hbm_copy_sweep.txt: 5.6-5.8 TB/s non-temporal
-// at 4-16 workgroups per CU, against 4.6-5.5 for grid-strided lanes). NT = non-temporal.
-template <bool NT>
+// The streaming copy, one 16-byte element per lane and one lane per element (n / 256
+// workgroups, no loop: MI355X_MICROARCH.md's float4 copy), non-temporal or default policy:
+// 6.49-6.53 TB/s read + write on MI355X at 1-8 GiB, against 5.4-5.8 for the 16 KiB
+// chunk-per-workgroup shape of rounds 1-5 (profiles/r6_hbm_copy.txt). MODE 0 copies, 1 only
+// reads (the xor of every element, kept live by a test that never passes), 2 only writes:
+// HBM writes stream at ~4.5-4.8 TB/s against ~6.9 for reads, which prices a write-heavy
+// kernel (the RS extension writes 3 bytes for every byte it reads).
+template <bool NT, int MODE>
 __global__ __launch_bounds__(256) void k_probe_copy(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
                                                     uint64_t n16) {
-  constexpr uint64_t kPer = 256 * 4;
-  for (uint64_t c = blockIdx.x; c * kPer < n16; c += gridDim.x) {
-    const uint64_t b = c * kPer + threadIdx.x;
-    if (b + 3 * 256 < n16) {
-      u32x4 v[4];
-#pragma unroll
-      for (int j = 0; j < 4; j++) v[j] = NT ? __builtin_nontemporal_load(src + b + j * 256) : src[b + j * 256];
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        if (NT)
-          __builtin_nontemporal_store(v[j], dst + b + j * 256);
-        else
-          dst[b + j * 256] = v[j];
-      }
-    } else {
-      for (uint64_t i = b; i < n16 && i < c * kPer + kPer; i += 256) dst[i] = src[i];
-    }
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (MODE == 2) {  // write only: grid-strided (a read-free stream needs few lanes in flight)
+    const u32x4 v = {(uint32_t)i, 1u, 2u, 3u};
+    for (uint64_t j = i; j < n16; j += (uint64_t)gridDim.x * 256) __builtin_nontemporal_store(v, dst + j);
+    return;
+  }
+  if (MODE == 1) {
+    u32x4 acc = {0, 0, 0, 0};
+    for (uint64_t j = i; j < n16; j += (uint64_t)gridDim.x * 256) acc ^= __builtin_nontemporal_load(src + j);
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9E3779B9u && i == 0) dst[0] = acc;
+    return;
+  }
+  if (i < n16) {
+    if (NT)
+      __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+    else
+      dst[i] = src[i];
   }
 }
 
@@ -76,13 +79,23 @@ hipError_t launch_probe_sha(uint32_t* out, unsigned long long* clk, uint32_t blo
   return hipGetLastError();
 }
 
-hipError_t launch_probe_copy(const void* src, void* dst, uint64_t bytes, uint32_t blocks, bool nt, hipStream_t s) {
-  if (nt)
-    hipLaunchKernelGGL(k_probe_copy<true>, dim3(blocks), dim3(256), 0, s, static_cast<const u32x4*>(src),
-                       static_cast<u32x4*>(dst), bytes / 16);
-  else
-    hipLaunchKernelGGL(k_probe_copy<false>, dim3(blocks), dim3(256), 0, s, static_cast<const u32x4*>(src),
-                       static_cast<u32x4*>(dst), bytes / 16);
+hipError_t launch_probe_copy(const void* src, void* dst, uint64_t bytes, uint32_t blocks, int mode, bool nt,
+                             hipStream_t s) {
+  const uint64_t n16 = bytes / 16;
+  const auto* sp = static_cast<const u32x4*>(src);
+  auto* dp = static_cast<u32x4*>(dst);
+  if (mode == 0) {
+    const uint64_t g = (n16 + 255) / 256;  // one lane per element
+    if (g > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    if (nt)
+      hipLaunchKernelGGL((k_probe_copy<true, 0>), dim3((unsigned)g), dim3(256), 0, s, sp, dp, n16);
+    else
+      hipLaunchKernelGGL((k_probe_copy<false, 0>), dim3((unsigned)g), dim3(256), 0, s, sp, dp, n16);
+  } else if (mode == 1) {
+    hipLaunchKernelGGL((k_probe_copy<true, 1>), dim3(blocks), dim3(256), 0, s, sp, dp, n16);
+  } else {
+    hipLaunchKernelGGL((k_probe_copy<true, 2>), dim3(blocks), dim3(256), 0, s, sp, dp, n16);
+  }
   return hipGetLastError();
 }
 

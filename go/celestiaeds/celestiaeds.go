@@ -108,11 +108,28 @@ type Context struct {
 	stageLen int
 }
 
+// maxKeptStage is the most page-locked staging a Context keeps between calls: one k = 512
+// ODS (512 x 512 x 512 B). Larger batches stage in a buffer of their own, freed after the call.
+const maxKeptStage = 512 * 512 * ShareSize
+
 // stagedLocked copies shares into the page-locked staging buffer and returns it, or a
-// C.malloc'd copy (release != nil: the caller frees it) when page-locked memory is not to
-// be had. The caller holds c.mu.
+// buffer of this call's own (release != nil: the caller frees it) for a batch above
+// maxKeptStage or when page-locked memory is not to be had. The caller holds c.mu.
 func (c *Context) stagedLocked(shares [][]byte) (buf unsafe.Pointer, release func()) {
 	need := len(shares) * ShareSize
+	if need > maxKeptStage {
+		// a batch beyond one k = 512 ODS: page-locked for this call only, so a replay of many
+		// squares does not leave that much host memory pinned for the Context's lifetime
+		buf = C.cel_host_alloc(C.size_t(need))
+		if buf != nil {
+			release = func() { C.cel_host_free(buf) }
+		} else {
+			buf = C.malloc(C.size_t(need))
+			release = func() { C.free(buf) }
+		}
+		copyShares(unsafe.Slice((*byte)(buf), need), shares)
+		return buf, release
+	}
 	if c.stageLen < need {
 		if c.stage != nil {
 			C.cel_host_free(c.stage)

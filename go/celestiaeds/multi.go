@@ -8,6 +8,7 @@ import "C"
 
 import (
 	"fmt"
+	"sort"
 	"unsafe"
 
 	"github.com/celestiaorg/celestia-app/v3/pkg/wrapper"
@@ -46,23 +47,32 @@ func (g *Group) Close() {
 }
 
 // handles returns the cel_ctx pointers in C memory (cgo may not pass a Go slice of C
-// pointers that the callee keeps) and a release func. Every Context's lock is held until
-// release: the library call uses all of them.
+// pointers that the callee keeps) and a release func. Every distinct Context's lock is held
+// until release (the library call uses all of them), taken in one fixed order (by the
+// cel_ctx address, whatever the slice order), so two Groups sharing Contexts in different
+// orders cannot deadlock.
 func (g *Group) handles() (**C.cel_ctx, func()) {
 	n := len(g.Ctxs)
 	arr := (**C.cel_ctx)(C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(uintptr(0)))))
 	s := unsafe.Slice(arr, n)
-	locked := map[*Context]bool{}
+	seen := map[*Context]bool{}
+	var distinct []*Context
 	for i, c := range g.Ctxs {
 		s[i] = c.ctx
-		if !locked[c] {
-			c.mu.Lock()
-			locked[c] = true
+		if !seen[c] {
+			seen[c] = true
+			distinct = append(distinct, c)
 		}
 	}
+	sort.Slice(distinct, func(a, b int) bool {
+		return uintptr(unsafe.Pointer(distinct[a].ctx)) < uintptr(unsafe.Pointer(distinct[b].ctx))
+	})
+	for _, c := range distinct {
+		c.mu.Lock()
+	}
 	return arr, func() {
-		for c := range locked {
-			c.mu.Unlock()
+		for i := len(distinct) - 1; i >= 0; i-- {
+			distinct[i].mu.Unlock()
 		}
 		C.free(unsafe.Pointer(arr))
 	}

@@ -256,12 +256,17 @@ cel_status cel_extend_batch_multi(cel_ctx* const* ctxs, uint32_t ngpu, const uin
  * chained in registers on every lane with no memory traffic (G compressions/s, best of 5
  * launches) and reports the sustained shader clock over that launch (MHz, nullable: shader
  * clock ticks per constant-rate tick of every wave); cel_probe_hbm_copy streams a copy over
- * `bytes` of HBM (half read, half written) and reports read + write GB/s (best of 5);
+ * `bytes` of HBM (half read, half written; one 16-byte element per lane) and reports read +
+ * write GB/s (best of 5); cel_probe_hbm_stream adds the read-only and write-only rates over
+ * the same half (each nullable: HBM writes stream slower than reads, which prices a
+ * write-heavy kernel such as the extension, 3 bytes written per byte read);
  * cel_probe_rs_transform runs the encode tile (GF(2^8): k = 32, 64 or 128; GF(2^16): k = 256
  * or 512) with its HBM traffic taken away and reports the microseconds one square's
  * extension (3k axis encodes) spends in the transform alone, whole chip (best of 5). */
 cel_status cel_probe_sha256(cel_ctx* ctx, double* g_compressions_per_s, double* shader_mhz);
 cel_status cel_probe_hbm_copy(cel_ctx* ctx, uint64_t bytes, double* gbps);
+cel_status cel_probe_hbm_stream(cel_ctx* ctx, uint64_t bytes, double* copy_gbps, double* read_gbps,
+                                double* write_gbps);
 cel_status cel_probe_rs_transform(cel_ctx* ctx, uint32_t k, double* us_per_square);
 
 /* ------------------------------------------------------ rsmt2d.Codec surface

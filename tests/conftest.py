@@ -12,6 +12,15 @@ import sys
 import numpy as np
 import pytest
 
+try:
+    # PyTorch before the library: torch brings its own HIP runtime, and the library (loaded
+    # by ctypes) then binds to that same runtime, as in bench.py. Loaded the other way
+    # round, torch's CUDA init reports "No HIP GPUs are available" in the same process
+    # (tests/test_gpu_bench_shapes.py after a ctypes test, profiles/r6_torch_order.txt).
+    import torch  # noqa: F401
+except ImportError:  # the CPU suite without torch still runs
+    pass
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (os.path.join(ROOT, "celestia-app_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
     if p not in sys.path:

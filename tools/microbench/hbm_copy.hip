@@ -51,6 +51,49 @@ __global__ __launch_bounds__(256) void k_chunk(const u32x4* __restrict__ s, u32x
   }
 }
 
+// round 6: the canonical float4 copy (one element per thread, one thread per element, no
+// loop: n / 256 workgroups), and read-only / write-only streams of the same shape
+template <bool NT>
+__global__ __launch_bounds__(256) void k_flat(const u32x4* __restrict__ s, u32x4* __restrict__ d, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) {
+    if (NT) __builtin_nontemporal_store(__builtin_nontemporal_load(s + i), d + i);
+    else d[i] = s[i];
+  }
+}
+__global__ __launch_bounds__(256) void k_read(const u32x4* __restrict__ s, u32x4* __restrict__ d, uint64_t n) {
+  const uint64_t st = (uint64_t)gridDim.x * 256;
+  u32x4 acc = {0, 0, 0, 0};
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += st) acc ^= __builtin_nontemporal_load(s + i);
+  if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) d[0] = acc;  // keeps the loads live
+}
+__global__ __launch_bounds__(256) void k_write(const u32x4* __restrict__ s, u32x4* __restrict__ d, uint64_t n) {
+  const uint64_t st = (uint64_t)gridDim.x * 256;
+  const u32x4 v = {(uint32_t)threadIdx.x, 1u, 2u, 3u};
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += st) __builtin_nontemporal_store(v, d + i);
+}
+
+template <class K>
+static float time_grid(K kern, dim3 grid, const u32x4* s, u32x4* d, uint64_t n) {
+  hipLaunchKernelGGL(kern, grid, dim3(256), 0, 0, s, d, n);
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  float best = 1e30f;
+  for (int r = 0; r < 5; r++) {
+    CK(hipEventRecord(a));
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, 0, s, d, n);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    if (ms < best) best = ms;
+  }
+  CK(hipEventDestroy(a));
+  CK(hipEventDestroy(b));
+  return best;
+}
+
 template <class K>
 static void run(const char* name, K kern, int wgcu, const u32x4* s, u32x4* d, uint64_t n) {
   dim3 grid(256 * wgcu), block(256);
@@ -81,6 +124,20 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&d, half));
   CK(hipMemset(s, 0x5A, half));
   CK(hipDeviceSynchronize());
+  {
+    const dim3 flat((unsigned)((n + 255) / 256));
+    float ms = time_grid(k_flat<false>, flat, s, d, n);
+    printf("%-22s          : %8.3f ms  %7.0f GB/s\n", "flat float4 default", ms, 2.0 * n * 16 / (ms * 1e-3) / 1e9);
+    ms = time_grid(k_flat<true>, flat, s, d, n);
+    printf("%-22s          : %8.3f ms  %7.0f GB/s\n", "flat float4 nt", ms, 2.0 * n * 16 / (ms * 1e-3) / 1e9);
+    for (int w : {4, 8, 16}) {
+      ms = time_grid(k_read, dim3(256 * w), s, d, n);
+      printf("%-22s WG/CU %2d: %8.3f ms  %7.0f GB/s (read only)\n", "read nt", w, ms, 1.0 * n * 16 / (ms * 1e-3) / 1e9);
+      ms = time_grid(k_write, dim3(256 * w), s, d, n);
+      printf("%-22s WG/CU %2d: %8.3f ms  %7.0f GB/s (write only)\n", "write nt", w, ms, 1.0 * n * 16 / (ms * 1e-3) / 1e9);
+    }
+  }
+  if (argc > 2) return 0;  // the flat / read / write lines only
   for (int w : {4, 8, 16}) {
     run("stride U1 default", k_stride<1, false>, w, s, d, n);
     run("stride U4 default", k_stride<4, false>, w, s, d, n);
