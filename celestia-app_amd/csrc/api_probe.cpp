@@ -101,11 +101,12 @@ cel_status cel_probe_hbm_stream(cel_ctx* ctx, uint64_t bytes, double* copy_gbps,
     e = best_time([&] { return launch_probe_copy(src, dst, half, 0, 0, v == 0, ctx->stream); }, 5, ctx->stream, &t);
     secs = std::min(secs, t);
   }
-  // read-only and write-only streams over the same half: the fastest of 4 / 8 / 16 workgroups per CU
+  // read-only and write-only streams over the same half: the fastest of 4 / 8 / 16 workgroups
+  // per CU (writes: also of 16 or 4 bytes per lane)
   double rsecs = 1e30, wsecs = 1e30;
-  for (int v = 0; v < 6 && e == hipSuccess && (read_gbps || write_gbps); v++) {
-    const int mode = v < 3 ? 1 : 2;
-    if ((mode == 1 && !read_gbps) || (mode == 2 && !write_gbps)) continue;
+  for (int v = 0; v < 9 && e == hipSuccess && (read_gbps || write_gbps); v++) {
+    const int mode = v < 3 ? 1 : v < 6 ? 2 : 3;
+    if ((mode == 1 && !read_gbps) || (mode != 1 && !write_gbps)) continue;
     const uint32_t blocks = (uint32_t)cus * (4u << (v % 3));
     double t = 0;
     e = best_time([&] { return launch_probe_copy(src, dst, half, blocks, mode, true, ctx->stream); }, 5, ctx->stream,

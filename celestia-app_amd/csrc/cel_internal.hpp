@@ -171,7 +171,7 @@ hipError_t launch_shard_finish(const uint32_t* gathered, uint32_t k, uint32_t nr
 // clk: 2 counters per wave), and a streaming copy of `bytes` (a multiple of 16).
 hipError_t launch_probe_sha(uint32_t* out, unsigned long long* clk, uint32_t blocks, int n, hipStream_t s);
 // mode 0: copy `bytes` from src to dst (one lane per 16-byte element; blocks unused); 1: read
-// src only; 2: write dst only (grid-strided over `blocks` workgroups)
+// src only; 2 / 3: write dst only, 16 / 4 bytes per lane (grid-strided over `blocks` workgroups)
 hipError_t launch_probe_copy(const void* src, void* dst, uint64_t bytes, uint32_t blocks, int mode, bool nt,
                              hipStream_t s);
 // GF(2^8) encode transform alone (rs_axis.hip), k = 32/64/128: ntiles tiles reading the same

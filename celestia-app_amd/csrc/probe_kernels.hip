@@ -48,9 +48,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // workgroups, no loop: MI355X_MICROARCH.md's float4 copy), non-temporal or default policy:
 // 6.49-6.53 TB/s read + write on MI355X at 1-8 GiB, against 5.4-5.8 for the 16 KiB
 // chunk-per-workgroup shape of rounds 1-5 (profiles/r6_hbm_copy.txt). MODE 0 copies, 1 only
-// reads (the xor of every element, kept live by a test that never passes), 2 only writes:
-// HBM writes stream at ~4.5-4.8 TB/s against ~6.9 for reads, which prices a write-heavy
-// kernel (the RS extension writes 3 bytes for every byte it reads).
+// reads (the xor of every element, kept live by a test that never passes), 2 and 3 only
+// write (16 / 4 bytes per lane): HBM writes stream at ~5.5 TB/s at best against ~7 for
+// reads, which prices a write-heavy kernel (the RS extension writes 3 bytes per byte read).
 template <bool NT, int MODE>
 __global__ __launch_bounds__(256) void k_probe_copy(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
                                                     uint64_t n16) {
@@ -58,6 +58,12 @@ __global__ __launch_bounds__(256) void k_probe_copy(const u32x4* __restrict__ sr
   if (MODE == 2) {  // write only: grid-strided (a read-free stream needs few lanes in flight)
     const u32x4 v = {(uint32_t)i, 1u, 2u, 3u};
     for (uint64_t j = i; j < n16; j += (uint64_t)gridDim.x * 256) __builtin_nontemporal_store(v, dst + j);
+    return;
+  }
+  if (MODE == 3) {  // write only, 4 bytes per lane (the RS kernels' store width): 5.5-5.6 TB/s
+    // against 4.0-4.6 for 16 bytes per lane (profiles/r6_hbm_write.txt)
+    uint32_t* d4 = reinterpret_cast<uint32_t*>(dst);
+    for (uint64_t j = i; j < 4 * n16; j += (uint64_t)gridDim.x * 256) d4[j] = (uint32_t)j;
     return;
   }
   if (MODE == 1) {
@@ -93,8 +99,10 @@ hipError_t launch_probe_copy(const void* src, void* dst, uint64_t bytes, uint32_
       hipLaunchKernelGGL((k_probe_copy<false, 0>), dim3((unsigned)g), dim3(256), 0, s, sp, dp, n16);
   } else if (mode == 1) {
     hipLaunchKernelGGL((k_probe_copy<true, 1>), dim3(blocks), dim3(256), 0, s, sp, dp, n16);
-  } else {
+  } else if (mode == 2) {
     hipLaunchKernelGGL((k_probe_copy<true, 2>), dim3(blocks), dim3(256), 0, s, sp, dp, n16);
+  } else {
+    hipLaunchKernelGGL((k_probe_copy<false, 3>), dim3(blocks), dim3(256), 0, s, sp, dp, n16);
   }
   return hipGetLastError();
 }

@@ -73,6 +73,26 @@ __global__ __launch_bounds__(256) void k_write(const u32x4* __restrict__ s, u32x
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += st) __builtin_nontemporal_store(v, d + i);
 }
 
+// write-only forms: 16 B or 4 B per lane, non-temporal or default policy, grid-strided
+template <int W, bool NT>
+__global__ __launch_bounds__(256) void k_write_form(const u32x4* __restrict__ s, u32x4* __restrict__ d, uint64_t n) {
+  const uint64_t st = (uint64_t)gridDim.x * 256;
+  if (W == 16) {
+    const u32x4 v = {(uint32_t)threadIdx.x, 1u, 2u, 3u};
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += st) {
+      if (NT) __builtin_nontemporal_store(v, d + i);
+      else d[i] = v;
+    }
+  } else {
+    uint32_t* d4 = reinterpret_cast<uint32_t*>(d);
+    const uint32_t v = threadIdx.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < 4 * n; i += st) {
+      if (NT) __builtin_nontemporal_store(v, d4 + i);
+      else d4[i] = v;
+    }
+  }
+}
+
 template <class K>
 static float time_grid(K kern, dim3 grid, const u32x4* s, u32x4* d, uint64_t n) {
   hipLaunchKernelGGL(kern, grid, dim3(256), 0, 0, s, d, n);
@@ -136,6 +156,14 @@ int main(int argc, char** argv) {
       ms = time_grid(k_write, dim3(256 * w), s, d, n);
       printf("%-22s WG/CU %2d: %8.3f ms  %7.0f GB/s (write only)\n", "write nt", w, ms, 1.0 * n * 16 / (ms * 1e-3) / 1e9);
     }
+  }
+  for (int w : {4, 8, 16}) {
+    float ms = time_grid(k_write_form<16, false>, dim3(256 * w), s, d, n);
+    printf("%-22s WG/CU %2d: %8.3f ms  %7.0f GB/s (write only)\n", "write x4 default", w, ms, 1.0 * n * 16 / (ms * 1e-3) / 1e9);
+    ms = time_grid(k_write_form<4, true>, dim3(256 * w), s, d, n);
+    printf("%-22s WG/CU %2d: %8.3f ms  %7.0f GB/s (write only)\n", "write dword nt", w, ms, 1.0 * n * 16 / (ms * 1e-3) / 1e9);
+    ms = time_grid(k_write_form<4, false>, dim3(256 * w), s, d, n);
+    printf("%-22s WG/CU %2d: %8.3f ms  %7.0f GB/s (write only)\n", "write dword default", w, ms, 1.0 * n * 16 / (ms * 1e-3) / 1e9);
   }
   if (argc > 2) return 0;  // the flat / read / write lines only
   for (int w : {4, 8, 16}) {
