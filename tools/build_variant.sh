@@ -3,7 +3,7 @@
 # no A/B knobs: a variant is a patch against celestia-app_amd/csrc (paths as `git diff`
 # prints them) applied to a copy of the sources, plus optional extra compile flags:
 #   bash tools/build_variant.sh <name> [<patch file> | -] ["<flags>"]  ->  variants/lib<name>.so
-# (tools/gpu_variants.sh times variants on the GPU box; build_variants/ and variants/ are
+# (tools/gpu_ab.sh times variants on the GPU box; build_variants/ and variants/ are
 # git-ignored.)
 set -e
 name=$1; patch=${2:--}; flags=$3
