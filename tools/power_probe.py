@@ -1,7 +1,8 @@
 """Socket power and shader clock while one pipeline phase runs back to back (rocm-smi
 sampled from a thread), to tell a power-capped phase from an issue- or HBM-bound one:
-  python tools/power_probe.py --phase extend|commit|probe --k 128 --batch 256 [--secs 6]
-CEL_EDS_LIB picks a variant build. 'probe' loops cel_probe_rs_transform (VALU only)."""
+  python tools/power_probe.py --phase extend|commit|probe|step --k 128 --batch 256 [--secs 6]
+CEL_EDS_LIB picks a variant build. 'probe' loops cel_probe_rs_transform (VALU only); 'step'
+the bench's step (four batches in flight, each extended and committed in turn)."""
 import argparse
 import ctypes
 import json
@@ -29,7 +30,16 @@ sb = SquareBatch(a.batch, a.k, ods_in_eds=True)
 sb.load_ods(torch.from_numpy(np.stack([random_ods(a.k, 1)] * a.batch)))
 sb.extend_and_commit()
 torch.cuda.synchronize()
-if a.phase == "probe":
+if a.phase == "step":  # the bench's step: 4 batches in flight, each extended and committed in turn
+    sbs = [sb] + [SquareBatch(a.batch, a.k, ods_in_eds=True) for _ in range(3)]
+    for b in sbs[1:]:
+        b.load_ods(torch.from_numpy(np.stack([random_ods(a.k, 2)] * a.batch)))
+    it = [0]
+
+    def fn():
+        sbs[it[0] % 4].extend_and_commit(caller_stream=True)
+        it[0] += 1
+elif a.phase == "probe":
     us = ctypes.c_double()
     fn = lambda: sb.ctx.lib.cel_probe_rs_transform(sb.ctx.handle, a.k, ctypes.byref(us))  # noqa: E731
 else:
