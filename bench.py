@@ -777,6 +777,18 @@ def measure_probe(ctx):
     return probe(ctx, 4 << 30)
 
 
+def achievable_mix(traffic, probe, k):
+    """The RS extension's own HBM ceiling, as algorithmic GB/s: its measured read and write
+    bytes per square (`traffic`, from the PMC profile) at the box's read-only and write-only
+    stream rates (`probe`: HBM writes stream ~25 % slower than reads), i.e. the rate the
+    extension would reach if its HBM time were the whole launch. None without the inputs."""
+    if not traffic or not probe or not probe.get("hbm_read_gbps") or not probe.get("hbm_write_gbps"):
+        return None
+    t_sq = traffic["read_per_square"] / (probe["hbm_read_gbps"] * 1e9) + \
+        traffic["write_per_square"] / (probe["hbm_write_gbps"] * 1e9)
+    return 2048 * k * k / t_sq / 1e9
+
+
 def step_ceiling(k, probe, secs_per_square):
     """The whole step against the VALU time of its two instruction streams, both same-run:
     the square's NMT compressions at the SHA-256 probe's rate plus its GF(2^8) extension's
@@ -1248,13 +1260,8 @@ def main():
         result["roofline"]["achievable"] = probe["hbm_copy_gbps"]
         result["roofline"]["achievable_basis"] = "cel_probe_hbm_copy: float4 streaming copy, one element per lane"
         result["roofline"]["frac_of_achievable_hbm"] = rs_gbs / probe["hbm_copy_gbps"]
-        tr = result["roofline"]["traffic"]
-        if tr and probe.get("hbm_read_gbps") and probe.get("hbm_write_gbps"):
-            # the extension's own mix: its measured read and write bytes at this box's read-only
-            # and write-only stream rates (HBM writes stream ~30 % slower than reads)
-            t_sq = tr["read_per_square"] / (probe["hbm_read_gbps"] * 1e9) + \
-                tr["write_per_square"] / (probe["hbm_write_gbps"] * 1e9)
-            mix = 2048 * k * k / t_sq / 1e9
+        mix = achievable_mix(result["roofline"]["traffic"], probe, k)
+        if mix:
             result["roofline"]["achievable_mix"] = mix
             result["roofline"]["frac_of_achievable_mix"] = rs_gbs / mix
             result["roofline"]["achievable_mix_basis"] = ("algorithmic bytes over the time the measured traffic "

@@ -70,3 +70,22 @@ def test_step_ceiling_fields():
     assert bench._step_fields(512, probe, 1e-3) == {} and bench._step_fields(128, None, 1e-3) == {}
     f = bench._step_fields(128, probe, 45e-6)
     assert abs(f["step_valu_frac"] - s["frac"]) < 1e-12 and f["step_rs_transform_us"] == 7.5
+
+
+def test_rs_traffic_and_achievable_mix():
+    """roofline.traffic splits the committed PMC profile into read and write bytes per square
+    (FETCH_SIZE doubled, WRITE_SIZE), and achievable_mix prices them at the probe's read-only
+    and write-only rates (bench.achievable_mix)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    tr = bench._rs_traffic(128, 256, "eds")
+    assert tr is not None and tr["bytes"] == tr["per_square"] * 256
+    assert abs(tr["read_per_square"] + tr["write_per_square"] - tr["per_square"]) < 0.03 * tr["per_square"]
+    assert tr["write_per_square"] > tr["read_per_square"]  # Q1..Q3 written, Q0 + Q1 read
+    probe = {"hbm_read_gbps": 7000.0, "hbm_write_gbps": 5000.0}
+    mix = bench.achievable_mix(tr, probe, 128)
+    t = tr["read_per_square"] / 7e12 + tr["write_per_square"] / 5e12
+    assert abs(mix - 2048 * 128 * 128 / t / 1e9) < 1e-6
+    assert 4000 < mix < 6000
+    assert bench.achievable_mix(tr, {"hbm_copy_gbps": 6000.0}, 128) is None
+    assert bench.achievable_mix(None, probe, 128) is None
