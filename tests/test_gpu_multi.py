@@ -249,6 +249,9 @@ def test_probes(ctx):
     assert 10 < p["sha256_gcomp_per_s"] < 60
     assert 800 < p["shader_mhz"] < 3000
     assert 1000 < p["hbm_copy_gbps"] < 8000
+    # round 6: the read-only and write-only streams (writes stream slower than reads on
+    # MI355X, profiles/r6_hbm_write.txt)
+    assert 1000 < p["hbm_write_gbps"] < p["hbm_read_gbps"] < 8000
     # the transform alone at k = 128: round 2 measured 8.47 us per square (profiles/r2_gf8_transform_only.log)
     assert 4 < p["rs_transform_us_k128"] < 16 and p["rs_transform_us_k64"] < p["rs_transform_us_k128"]
     # GF(2^16) k = 512: round 2 measured 278.5 us per square (profiles/r2_gf16_transform_only.txt)
