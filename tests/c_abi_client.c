@@ -7,7 +7,9 @@
  * "not a power of 2" error string of :68. Then the multi-GPU entry points as the Go Group
  * (go/celestiaeds/multi.go) calls them, with two ctxs on device 0: cel_extend_batch_multi on
  * three copies of that square (each DAH = the known answer), and cel_extend_sharded on a
- * k = 256 square (one rank, the "local" plan) against cel_extend_shares on the same shares.
+ * k = 256 square (one rank, the "local" plan) against cel_extend_shares on the same shares,
+ * then that square through an explicit two-rank plan with CEL_FLAG_SHARD_PEERCOPY (transport
+ * "copy", no note) and its all-to-all timed alone (cel_shard_plan_time_exchange).
  * Exit codes: 0 = all checks passed; 2 = no device (CEL_EDEVICE from cel_ctx_create:
  * the library fails loudly, there is no CPU fallback); 1 = a check failed.
  */
@@ -96,6 +98,25 @@ int main(void) {
   printf("sharded k=256: status %d / %d dah %s\n", st, st2, h);
   ok &= st == CEL_OK && st2 == CEL_OK && memcmp(daha, dahb, 32) == 0;
   ok &= memcmp(rra, rrb, (size_t)2 * WB * CEL_NMT_NODE_SIZE) == 0; /* row and column roots */
+  /* round 6: the same square through an explicit two-rank plan that never starts RCCL
+   * (CEL_FLAG_SHARD_PEERCOPY; both ctxs on device 0, so transport "copy"), its exchange timed
+   * alone, and the roots against cel_extend_shares again */
+  cel_shard_plan* plan = NULL;
+  st = cel_shard_plan_create(group, 2, KB, CEL_FLAG_ORDER_CHECK | CEL_FLAG_SHARD_PEERCOPY, &plan);
+  ok &= st == CEL_OK && plan != NULL;
+  if (plan) {
+    double a2a_us = 0;
+    st = cel_shard_plan_upload(plan, big);
+    if (st == CEL_OK) st = cel_shard_plan_run(plan);
+    if (st == CEL_OK) st = cel_shard_plan_wait(plan, NULL, rrb, crb, dahb);
+    cel_status st3x = cel_shard_plan_time_exchange(plan, 3, &a2a_us);
+    printf("plan k=256 x2: status %d transport %s note \"%s\" exchange %.1f us (%d)\n", st,
+           cel_shard_plan_transport(plan), cel_shard_plan_note(plan), a2a_us, st3x);
+    ok &= st == CEL_OK && strcmp(cel_shard_plan_transport(plan), "copy") == 0 && cel_shard_plan_note(plan)[0] == 0;
+    ok &= st3x == CEL_OK && a2a_us > 0;
+    ok &= memcmp(daha, dahb, 32) == 0 && memcmp(rra, rrb, (size_t)2 * WB * CEL_NMT_NODE_SIZE) == 0;
+    cel_shard_plan_destroy(plan);
+  }
   free(rra);
   free(big);
   cel_ctx_destroy(ctx2);
