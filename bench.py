@@ -123,6 +123,7 @@ def parse():
                          "distcheck: the launcher / rendezvous / timing contract on CPU ranks over gloo "
                          "(no GPU work; used by the CPU tests)")
     ap.add_argument("--no-host-io", action="store_true", help="skip the host_io (PCIe-inclusive) measurement")
+    ap.add_argument("--no-power", action="store_true", help="skip the rocm-smi power / clock reading of the phases")
     ap.add_argument("--repair-p", type=float, default=0.55, help="repair mode: cell survival probability")
     ap.add_argument("--repair-input", default="device", choices=["device", "host"],
                     help="repair mode: EDS resident in HBM (cel_dev_repair) or host buffers (cel_repair, PCIe)")
@@ -1061,6 +1062,54 @@ def _measure_batch(ctx, local, rank, k, B, steps, warmup, n_distinct, layout, ph
     return {"sb": sb, "distinct": distinct, "elapsed": elapsed, "t_ext": t_ext, "t_com": t_com}
 
 
+def measure_power(fn, secs=1.5):
+    """Median socket power (W) and shader clock (MHz) from rocm-smi while fn runs back to back
+    for `secs` (synchronised every 4 calls), or None fields when rocm-smi reads nothing."""
+    import threading
+    samples, stop = [], threading.Event()
+
+    def sampler():
+        time.sleep(0.3)
+        while not stop.is_set():
+            try:
+                out = subprocess.run(["rocm-smi", "-P", "-c", "--json"], capture_output=True, text=True,
+                                     timeout=10).stdout
+                samples.append(json.loads(out[out.index("{"):]))
+            except Exception:  # noqa: BLE001  (no rocm-smi, or no JSON: the fields stay None)
+                pass
+            time.sleep(0.2)
+
+    th = threading.Thread(target=sampler, daemon=True)
+    th.start()
+    t0, n = time.time(), 0
+    while time.time() - t0 < secs:
+        fn()
+        n += 1
+        if n % 4 == 0:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    stop.set()
+    th.join()
+    pw, mhz = [], []
+    for smp in samples:
+        for card in smp.values():
+            if not isinstance(card, dict):
+                continue
+            for key, val in card.items():
+                kl = key.lower()
+                try:
+                    if "power" in kl and "(w)" in kl:
+                        pw.append(float(val))
+                    elif kl.startswith("sclk"):
+                        f = float(str(val).strip("()Mhz "))
+                        if f > 100:  # skip the level index rocm-smi prints beside the clock
+                            mhz.append(f)
+                except ValueError:
+                    pass
+    med = lambda v: sorted(v)[len(v) // 2] if v else None  # noqa: E731
+    return {"watts": med(pw), "sclk_mhz": med(mhz), "samples": len(samples), "calls": n}
+
+
 def measure_host_io(ctx, k, n=16, reps=5):
     """cel_extend_batch over page-locked host buffers (cel_host_alloc): n ODSs in, then
     (a) the EDS + roots + DAH out (what rsmt2d.ImportExtendedDataSquare needs) and
@@ -1273,6 +1322,13 @@ def main():
         step = step_ceiling(k, probe, elapsed / (B * a.steps))
         if step:
             result["roofline_step"] = step
+    if world == 1 and not a.no_power:
+        # after the timed region: each phase looped ~1.5 s while rocm-smi reads socket power
+        # and the shader clock (the path runs in the board's power envelope)
+        _rider(result, "power", lambda: {"extend": measure_power(sb.extend_only),
+                                         "commit": measure_power(sb.commit_only),
+                                         "basis": "rocm-smi -P -c every ~0.3 s while the phase runs back to back "
+                                                  "on this batch (outside the timed region)"})
 
     if a.k == 128 and a.k512_batch > 0:
         # The metric names k=128 and k=512: a short GF(2^16) batch rides along with the
