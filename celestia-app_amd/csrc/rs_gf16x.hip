@@ -149,8 +149,8 @@ constexpr uint32_t shard_bits_a(uint32_t r) {
 // One radix-2 layer of arrangement A (layer D_LOG in 0..4) over w[2r] (a), w[2r+1] (b).
 // Groups run in two halves by register bit 5 (shard bit 8): the twiddle's gamma
 // coordinate cb is constant over a half (it only sees shard bit 8 and K), so the
-// lane-independent tables of cb and cb*p are built once per half.
-template <int LOGK, int D_LOG, bool IFFT, int NW>
+// lane-independent tables of cb and cb*p are built once per half. HS >= 0: half HS only.
+template <int LOGK, int D_LOG, bool IFFT, int HS, int NW>
 __device__ __forceinline__ void layer_a(uint32_t (&w)[NW], const Tb& g, uint32_t m7, uint32_t m3) {
   constexpr uint32_t K = 1u << LOGK;
   constexpr int NR = NW / 2;
@@ -162,7 +162,9 @@ __device__ __forceinline__ void layer_a(uint32_t (&w)[NW], const Tb& g, uint32_t
   sfor<NH>([&](auto hi) {
     constexpr int h = decltype(hi)::value;
     constexpr uint32_t cb = coord_b(tw(32 * h));
-    if constexpr (cb == 0) {
+    if constexpr (HS >= 0 && h != HS) {
+      // the other half: not in this call
+    } else if constexpr (cb == 0) {
       sfor<GPH>([&](auto gi) {
         constexpr int r0 = 32 * h + decltype(gi)::value * 2 * D;  // bit D_LOG clear, bits below zero
         constexpr uint32_t c = tw(r0);  // lane part added per lane
@@ -221,13 +223,14 @@ __device__ __forceinline__ void layer_a(uint32_t (&w)[NW], const Tb& g, uint32_t
 }
 
 // Register bit RB (2, 3, 4) <-> lane bit RB + 1 (8, 16, 32 lanes apart): a 2x2 transpose
-// of every register pair (r, r | 1 << RB), for both coordinates. An involution.
-template <int RB, int NW>
+// of every register pair (r, r | 1 << RB), for both coordinates. An involution. HS >= 0:
+// the registers of half HS (register bit 5) only.
+template <int RB, int HS, int NW>
 __device__ __forceinline__ void swap_bit(uint32_t (&w)[NW]) {
   constexpr int NR = NW / 2;
   sfor<NR>([&](auto ri) {
     constexpr int r = decltype(ri)::value;
-    if constexpr (!((r >> RB) & 1)) {
+    if constexpr (!((r >> RB) & 1) && (HS < 0 || (r >> 5) == HS)) {
       constexpr int r1 = r | (1 << RB);
       sfor<2>([&](auto ci) {
         constexpr int u = 2 * r + decltype(ci)::value, v = 2 * r1 + decltype(ci)::value;
@@ -260,14 +263,23 @@ __device__ __forceinline__ void pmuladd(uint32_t (&w)[NW]) {
   }
 }
 
-// Arrangement B: block b = registers 4b..4b+3 = w[8b..8b+8), shard bits 5.. = b.
-template <int LOGK, int NW>
-__device__ __forceinline__ void stage_b(uint32_t (&w)[NW]) {
+// Arrangement B: block b = registers 4b..4b+3 = w[8b..8b+8), shard bits 5.. = b; block b
+// lies in half b >> 3 (register bit 5). stage_b_in: the bit transposes and the IFFT layers
+// 5 .. LOGK-2 (block groups of at most 8, inside one half), for half HS (all if HS < 0);
+// stage_b_mid: the merged last-IFFT / first-FFT layer (K = 512: across the halves);
+// stage_b_out: the FFT layers LOGK-2 .. 5 and the transposes back, for half HS.
+template <int HS, int B>
+constexpr bool in_half() { return HS < 0 || (B >> 3) == HS; }
+
+template <int LOGK, int HS, int NW>
+__device__ __forceinline__ void stage_b_in(uint32_t (&w)[NW]) {
   constexpr uint32_t K = 1u << LOGK;
   constexpr int NB = NW / 8;
   sfor<NB>([&](auto b) {
-    tr8<8 * decltype(b)::value>(w);
-    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (in_half<HS, decltype(b)::value>()) {
+      tr8<8 * decltype(b)::value>(w);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   });
   // IFFT layers 5 .. LOGK-2
   sfor<LOGK - 6>([&](auto t) {
@@ -275,45 +287,60 @@ __device__ __forceinline__ void stage_b(uint32_t (&w)[NW]) {
     constexpr int DB = 1 << (d - 5);  // block distance
     sfor<NB / (2 * DB)>([&](auto gi) {
       constexpr int b0 = decltype(gi)::value * 2 * DB;
-      constexpr uint32_t c = ifft_tw(K, d, (uint32_t)b0 << 5);
-      sfor<DB>([&](auto ji) {
-        constexpr int x = 8 * (b0 + decltype(ji)::value), y = x + 8 * DB;
-        pxor<x, y>(w);
-        pmuladd<c, x, y>(w);
-        __builtin_amdgcn_sched_barrier(0);
-      });
+      if constexpr (in_half<HS, b0>()) {
+        constexpr uint32_t c = ifft_tw(K, d, (uint32_t)b0 << 5);
+        sfor<DB>([&](auto ji) {
+          constexpr int x = 8 * (b0 + decltype(ji)::value), y = x + 8 * DB;
+          pxor<x, y>(w);
+          pmuladd<c, x, y>(w);
+          __builtin_amdgcn_sched_barrier(0);
+        });
+      }
     });
   });
-  {  // last IFFT layer and first FFT layer act on the same pairs: one multiply by c1 + c2
-    constexpr int d = LOGK - 1;
-    constexpr int DB = 1 << (d - 5);
-    constexpr uint32_t c = ifft_tw(K, d, 0) ^ fft_tw(d, 0);
-    sfor<DB>([&](auto ji) {
-      constexpr int x = 8 * decltype(ji)::value, y = x + 8 * DB;
-      pxor<x, y>(w);
-      pmuladd<c, x, y>(w);
-      pxor<x, y>(w);
-      __builtin_amdgcn_sched_barrier(0);
-    });
-  }
+}
+
+template <int LOGK, int NW>
+__device__ __forceinline__ void stage_b_mid(uint32_t (&w)[NW]) {
+  // last IFFT layer and first FFT layer act on the same pairs: one multiply by c1 + c2
+  constexpr uint32_t K = 1u << LOGK;
+  constexpr int d = LOGK - 1;
+  constexpr int DB = 1 << (d - 5);
+  constexpr uint32_t c = ifft_tw(K, d, 0) ^ fft_tw(d, 0);
+  sfor<DB>([&](auto ji) {
+    constexpr int x = 8 * decltype(ji)::value, y = x + 8 * DB;
+    pxor<x, y>(w);
+    pmuladd<c, x, y>(w);
+    pxor<x, y>(w);
+    __builtin_amdgcn_sched_barrier(0);
+  });
+}
+
+template <int LOGK, int HS, int NW>
+__device__ __forceinline__ void stage_b_out(uint32_t (&w)[NW]) {
+  constexpr int NB = NW / 8;
   // FFT layers LOGK-2 .. 5
   sfor<LOGK - 6>([&](auto t) {
     constexpr int d = LOGK - 2 - decltype(t)::value;
     constexpr int DB = 1 << (d - 5);
     sfor<NB / (2 * DB)>([&](auto gi) {
       constexpr int b0 = decltype(gi)::value * 2 * DB;
-      constexpr uint32_t c = fft_tw(d, (uint32_t)b0 << 5);
-      sfor<DB>([&](auto ji) {
-        constexpr int x = 8 * (b0 + decltype(ji)::value), y = x + 8 * DB;
-        pmuladd<c, x, y>(w);
-        pxor<x, y>(w);
-        __builtin_amdgcn_sched_barrier(0);
-      });
+      if constexpr (in_half<HS, b0>()) {
+        constexpr uint32_t c = fft_tw(d, (uint32_t)b0 << 5);
+        sfor<DB>([&](auto ji) {
+          constexpr int x = 8 * (b0 + decltype(ji)::value), y = x + 8 * DB;
+          pmuladd<c, x, y>(w);
+          pxor<x, y>(w);
+          __builtin_amdgcn_sched_barrier(0);
+        });
+      }
     });
   });
   sfor<NB>([&](auto b) {
-    tr8<8 * decltype(b)::value>(w);
-    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (in_half<HS, decltype(b)::value>()) {
+      tr8<8 * decltype(b)::value>(w);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   });
 }
 
@@ -323,14 +350,16 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
 
 // (lo, hi) -> (a, b): a = lo ^ A(hi), b = hi; the inverse is the same map. One table
 // materialisation for the whole array, one register's conversion at a time.
-template <int NW>
+template <int HS, int NW>
 __device__ __forceinline__ void convert(uint32_t (&w)[NW], uint32_t m7, uint32_t m3) {
   constexpr Tab8 t = tab_amap();
   const Tb tb{vconst<t.t0l>(), sconst<t.t0h>(), vconst<t.t1l>(), sconst<t.t1h>(), sconst<t.t2>()};
   sfor<NW / 2>([&](auto ri) {
     constexpr int i = decltype(ri)::value;
-    w[2 * i] = madd(w[2 * i], sel(w[2 * i + 1], m7, m3), tb);
-    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (HS < 0 || (i >> 5) == HS) {
+      w[2 * i] = madd(w[2 * i], sel(w[2 * i + 1], m7, m3), tb);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   });
 }
 
@@ -345,10 +374,11 @@ typedef uint32_t D2 __attribute__((ext_vector_type(2)));
 // 4-lane banks) turns each pair into (lo dword, hi dword) of the same 4 symbols and lane
 // bit 2 into a column bit; it is an involution, so the same exchange undoes it before
 // the stores.
-template <int NW>
+template <int HS, int NW>
 __device__ __forceinline__ void pair_lo_hi(uint32_t (&w)[NW]) {
   sfor<NW / 2>([&](auto ri) {
     constexpr int i = decltype(ri)::value;
+    if constexpr (HS >= 0 && (i >> 5) != HS) return;
     // banks 1, 3 (lane bit 2 set) take the partner's second dword into the first;
     // banks 0, 2 take the partner's first dword into the second
     const uint32_t lo = __builtin_amdgcn_update_dpp(w[2 * i], w[2 * i + 1], 0x124, 0xF, 0xA, false);
@@ -361,9 +391,9 @@ __device__ __forceinline__ void pair_lo_hi(uint32_t (&w)[NW]) {
 // Tile = (square z, axis x, 64-byte column cb): one wave. Shard j of the axis sits at
 // in + z*in_sq + x*in_axis + place(j) + 64*cb (see RsGeom; blocked placement for the
 // output and the data copy when blk_log != 0).
-// PROBE (cel_probe_rs_transform): the same tile whose stores run only when blk_log == 31,
-// which the probe never sets (a run-time test keeps the transform live); its geometry
-// points every load at one cache-resident 512-byte block.
+// PROBE (cel_probe_rs_transform): the same tile with its stores aimed past the buffer's
+// range (dropped by the buffer range check, so the transform stays live and nothing reaches
+// HBM); its geometry points every load at one cache-resident 512-byte block.
 template <int LOGK, bool CHECK = false, bool PROBE = false>
 __global__ __launch_bounds__(256, LOGK == 9 ? 3 : 4) void k_rs_gf16x(RsGeom g) {
   constexpr int K = 1 << LOGK;
@@ -419,52 +449,84 @@ __global__ __launch_bounds__(256, LOGK == 9 ? 3 : 4) void k_rs_gf16x(RsGeom g) {
       }
     }
   }
-  pair_lo_hi(w);
-  convert(w, m7, m3);  // -> (a, b)
-  // IFFT, arrangement A
-  layer_a<LOGK, 0, true>(w, lane_tab_here<5>(), m7, m3);
-  layer_a<LOGK, 1, true>(w, lane_tab_here<4>(), m7, m3);
-  layer_a<LOGK, 2, true>(w, lane_tab_here<3>(), m7, m3);
-  layer_a<LOGK, 3, true>(w, lane_tab_here<2>(), m7, m3);
-  layer_a<LOGK, 4, true>(w, lane_tab_here<1>(), m7, m3);
-  swap_bit<2>(w);
-  swap_bit<3>(w);
-  swap_bit<4>(w);
-  stage_b<LOGK>(w);
-  swap_bit<2>(w);
-  swap_bit<3>(w);
-  swap_bit<4>(w);
-  // FFT, arrangement A
-  layer_a<LOGK, 4, false>(w, lane_tab_here<1>(), m7, m3);
-  layer_a<LOGK, 3, false>(w, lane_tab_here<2>(), m7, m3);
-  layer_a<LOGK, 2, false>(w, lane_tab_here<3>(), m7, m3);
-  layer_a<LOGK, 1, false>(w, lane_tab_here<4>(), m7, m3);
-  layer_a<LOGK, 0, false>(w, lane_tab_here<5>(), m7, m3);
-  convert(w, m7, m3);  // -> (lo, hi)
-  pair_lo_hi(w);
+  // The transform. K = 512 runs half by half (register bit 5 = shard bit 8) where it can: both
+  // halves' loads are issued above, half 0 goes through the IFFT layers 0-7 while half 1's
+  // loads land, the merged layer 8 joins them, and half 0's FFT ends with its stores before
+  // half 1's FFT starts, so loads and stores overlap this wave's own arithmetic instead of
+  // bracketing it. K = 256 (one half) keeps the whole-array order.
+  constexpr int NHALF = LOGK == 9 ? 2 : 1;
+  auto front = [&](auto hs) {
+    constexpr int HS = decltype(hs)::value;
+    pair_lo_hi<HS>(w);
+    convert<HS>(w, m7, m3);  // -> (a, b)
+    // IFFT, arrangement A
+    layer_a<LOGK, 0, true, HS>(w, lane_tab_here<5>(), m7, m3);
+    layer_a<LOGK, 1, true, HS>(w, lane_tab_here<4>(), m7, m3);
+    layer_a<LOGK, 2, true, HS>(w, lane_tab_here<3>(), m7, m3);
+    layer_a<LOGK, 3, true, HS>(w, lane_tab_here<2>(), m7, m3);
+    layer_a<LOGK, 4, true, HS>(w, lane_tab_here<1>(), m7, m3);
+    swap_bit<2, HS>(w);
+    swap_bit<3, HS>(w);
+    swap_bit<4, HS>(w);
+    stage_b_in<LOGK, HS>(w);
+  };
   const auto rout = rsrc(g.out + (uint64_t)z * g.out_sq + (uint64_t)xa * g.out_axis);
   const uint32_t out_shard = (uint32_t)g.out_shard, out_blk = (uint32_t)g.out_blk;
-  // the lane's output offset from the lane id again: col and lane_bits held across the
-  // transform would cost two more VGPRs at the 168 the kernel runs at
-  uint32_t ln = threadIdx.x;
-  asm volatile("" : "+v"(ln));
-  ln &= 63u;
-  const uint32_t vout = place((ln >> 3) << 5, out_shard, out_blk) + cb * 64u + (ln & 7u) * 8u;
-  if constexpr (CHECK) {  // repair's encoding check: compare with the parity in place
-    uint32_t diff = 0;
+  uint32_t diff = 0;
+  auto back = [&](auto hs) {
+    constexpr int HS = decltype(hs)::value;
+    stage_b_out<LOGK, HS>(w);
+    swap_bit<2, HS>(w);
+    swap_bit<3, HS>(w);
+    swap_bit<4, HS>(w);
+    // FFT, arrangement A
+    layer_a<LOGK, 4, false, HS>(w, lane_tab_here<1>(), m7, m3);
+    layer_a<LOGK, 3, false, HS>(w, lane_tab_here<2>(), m7, m3);
+    layer_a<LOGK, 2, false, HS>(w, lane_tab_here<3>(), m7, m3);
+    layer_a<LOGK, 1, false, HS>(w, lane_tab_here<4>(), m7, m3);
+    layer_a<LOGK, 0, false, HS>(w, lane_tab_here<5>(), m7, m3);
+    convert<HS>(w, m7, m3);  // -> (lo, hi)
+    pair_lo_hi<HS>(w);
+    // the lane's output offset from the lane id again: col and lane_bits held across the
+    // transform would cost two more VGPRs at the 168 the kernel runs at
+    uint32_t ln = threadIdx.x;
+    asm volatile("" : "+v"(ln));
+    ln &= 63u;
+    const uint32_t vout = place((ln >> 3) << 5, out_shard, out_blk) + cb * 64u + (ln & 7u) * 8u;
+    constexpr int i0 = HS < 0 ? 0 : 32 * HS, i1 = HS < 0 ? NR : 32 * HS + 32;
+    if constexpr (CHECK) {  // repair's encoding check: compare with the parity in place
 #pragma unroll
-    for (int i = 0; i < NR; i++) {
-      const uint32_t so = __builtin_amdgcn_readfirstlane(place(reg_bits((uint32_t)i), out_shard, out_blk));
-      const auto v = __builtin_amdgcn_raw_buffer_load_b64(rout, vout, so, 0);
-      diff |= (v[0] ^ w[2 * i]) | (v[1] ^ w[2 * i + 1]);
+      for (int i = i0; i < i1; i++) {
+        const uint32_t so = __builtin_amdgcn_readfirstlane(place(reg_bits((uint32_t)i), out_shard, out_blk));
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rout, vout, so, 0);
+        diff |= (v[0] ^ w[2 * i]) | (v[1] ^ w[2 * i + 1]);
+      }
+      asm volatile("" : "+v"(diff));
+    } else {
+      // PROBE: the same stores aimed past the buffer's range (offset >= num_records: dropped),
+      // so the probe runs the encode's instruction stream without writing HBM
+      const uint32_t vo = PROBE ? 0x80000000u : vout;
+#pragma unroll
+      for (int i = i0; i < i1; i++) {
+        const uint32_t so = __builtin_amdgcn_readfirstlane(place(reg_bits((uint32_t)i), out_shard, out_blk));
+        __builtin_amdgcn_raw_buffer_store_b64(D2{w[2 * i], w[2 * i + 1]}, rout, vo, so, 0);
+      }
     }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  if constexpr (NHALF == 2) {
+    front(std::integral_constant<int, 0>{});
+    front(std::integral_constant<int, 1>{});
+    stage_b_mid<LOGK>(w);
+    back(std::integral_constant<int, 0>{});
+    back(std::integral_constant<int, 1>{});
+  } else {
+    front(std::integral_constant<int, -1>{});
+    stage_b_mid<LOGK>(w);
+    back(std::integral_constant<int, -1>{});
+  }
+  if constexpr (CHECK) {
     if (__any(diff != 0) && lane == 0) atomicOr(g.chk_flags + (g.chk_idx ? g.chk_idx[x] : (int32_t)x), 1);
-  } else if (!PROBE || g.blk_log == 31u) {
-#pragma unroll
-    for (int i = 0; i < NR; i++) {
-      const uint32_t so = __builtin_amdgcn_readfirstlane(place(reg_bits((uint32_t)i), out_shard, out_blk));
-      __builtin_amdgcn_raw_buffer_store_b64(D2{w[2 * i], w[2 * i + 1]}, rout, vout, so, 0);
-    }
   }
 }
 
