@@ -20,13 +20,16 @@
 // Two arrangements of the shard index s (K = 512; K = 256 drops bit 8):
 //   A: register r bits 0-4 = s bits 0-4, r bit 5 = s bit 8, lane L = s bits 5-7.
 //      Layers 0-4 (IFFT up, FFT down). Twiddle = compile-time part (register bits) XOR
-//      L << (5 - layer) (lane part, in GF(2^8)): v_perm product tables per lane, built
-//      by XORing the compile-time table with the lane's table of the layer.
+//      L << (5 - layer) (lane part, in GF(2^8)). Layers 0-1 (partners inside a block of
+//      4 registers): v_perm product tables per lane, built by XORing the compile-time
+//      table with the lane's table of the layer. Layers 2-4 (partners in different
+//      blocks, twiddles in GF(2^8)): on bit planes, as in B, the lane part added as
+//      XOR networks under lane masks (layer_p).
 //   B: register r bits 0-1 = s bits 0-1, r bits 2.. = s bits 5.., lane L = s bits 2-4.
 //      Layers 5..log2(K)-1 have compile-time twiddles in GF(2^8): four shards x 4
-//      symbols x (a, b) = 32 bytes share every twiddle, so each 8-dword block is turned
-//      into 8 bit planes (8x8 bit transpose) and a butterfly is 8 xors plus an 8x8 GF(2)
-//      matrix network of xor3 ops.
+//      symbols x (a, b) = 32 bytes share every twiddle, so each 8-dword block (turned
+//      into 8 bit planes by an 8x8 bit transpose before layer 2) is a butterfly of 8
+//      xors plus an 8x8 GF(2) matrix network of xor3 ops.
 //   A <-> B swaps register bits 2, 3, 4 with lane bits 3, 4, 5: DPP row_ror:8,
 //   v_permlane16_swap and v_permlane32_swap (a 2x2 transpose per register pair each).
 #include <hip/hip_runtime.h>
@@ -146,7 +149,8 @@ constexpr uint32_t shard_bits_a(uint32_t r) {
   return (r & 31u) | ((r >> 5) << 8);
 }
 
-// One radix-2 layer of arrangement A (layer D_LOG in 0..4) over w[2r] (a), w[2r+1] (b).
+// One radix-2 layer of arrangement A on bytes (layer D_LOG in 0..1 as shipped; 0..4 valid)
+// over w[2r] (a), w[2r+1] (b).
 // Groups run in two halves by register bit 5 (shard bit 8): the twiddle's gamma
 // coordinate cb is constant over a half (it only sees shard bit 8 and K), so the
 // lane-independent tables of cb and cb*p are built once per half. HS >= 0: half HS only.
@@ -222,6 +226,112 @@ __device__ __forceinline__ void layer_a(uint32_t (&w)[NW], const Tb& g, uint32_t
   });
 }
 
+// The lane's masks of the bits of L (all ones where the bit is set), from the lane id
+__device__ __forceinline__ void lane_masks(uint32_t& m0, uint32_t& m1, uint32_t& m2) {
+  uint32_t l = threadIdx.x;
+  asm volatile("" : "+v"(l));
+  const uint32_t L = (l & 63u) >> 3;
+  m0 = 0u - (L & 1u);
+  m1 = 0u - ((L >> 1) & 1u);
+  m2 = 0u - ((L >> 2) & 1u);
+}
+
+// Row R of x ^= (CA + lane part) * y, the lane part sum_j L_j * (1 << (S + j)): the
+// coefficient of plane y_k is c0 ^ parity(L & J) (c0 = bit k of CA's row, J = the e_j whose
+// rows have bit k). lane_group(key) = the planes k whose (J, c0) is (key >> 1, key & 1).
+template <uint32_t CA, int S, int R>
+constexpr uint32_t lane_group(int key) {
+  uint32_t g = 0;
+  for (int k = 0; k < 8; k++) {
+    uint32_t J = 0;
+    for (int j = 0; j < 3; j++) J |= ((mul_row8((1u << j) << S, R) >> k) & 1u) << j;
+    const uint32_t c0 = (mul_row8(CA, R) >> k) & 1u;
+    if ((int)(J * 2 + c0) == key) g |= 1u << k;
+  }
+  return g;
+}
+
+// planes w[XO..XO+8) ^= (CA + lane part) * planes w[YO..YO+8): per row, the planes of one
+// coefficient class are XORed together and added under that class's lane mask M[J] (or its
+// complement when c0 is set) by one v_bitop3; the class (J = 0, c0 = 1) is added plainly.
+template <uint32_t CA, int S, int XO, int YO, int NW>
+__device__ __forceinline__ void pmuladd_lane(uint32_t (&w)[NW], const uint32_t (&M)[8]) {
+  sfor<8>([&](auto ri) {
+    constexpr int r = decltype(ri)::value;
+    sfor<16>([&](auto ki) {
+      constexpr int key = decltype(ki)::value;
+      constexpr uint32_t g = lane_group<CA, S, r>(key);
+      if constexpr (key == 1 && g != 0) {
+        xrow<g, YO, 0>(w[XO + r], w);
+      } else if constexpr (key > 1 && g != 0) {
+        constexpr int k0 = __builtin_ctz(g);
+        uint32_t q = w[YO + k0];
+        xrow<g & ~(1u << k0), YO, 0>(q, w);
+        if constexpr (key & 1) {
+          w[XO + r] = __builtin_amdgcn_bitop3_b32(w[XO + r], M[key >> 1], q, 0xD2);  // x ^ (~m & q)
+        } else {
+          w[XO + r] = __builtin_amdgcn_bitop3_b32(w[XO + r], M[key >> 1], q, 0x78);  // x ^ (m & q)
+        }
+      }
+    });
+  });
+}
+
+// planes w[XO..XO+8) ^= C * planes w[YO..YO+8) (C < 256; C == 0 adds nothing)
+template <uint32_t C, int XO, int YO, int NW>
+__device__ __forceinline__ void pmuladd(uint32_t (&w)[NW]) {
+  if constexpr (C != 0) {
+    sfor<8>([&](auto r) { xrow<mul_row8(C, decltype(r)::value), YO, 0>(w[XO + decltype(r)::value], w); });
+  }
+}
+
+template <int HS, int B>
+constexpr bool in_half() { return HS < 0 || (B >> 3) == HS; }
+
+// Layers 2-4 of arrangement A on bit planes. Their twiddles lie in GF(2^8) (coord_b 0):
+// c = ca (register bits, compile-time) + L0*e0 + L1*e1 + L2*e2 with e_j = 1 << (S + j),
+// S = 5 - layer (the lane part, linear in L's bits), so x ^= c*y is the compile-time network
+// of ca plus the three networks of e_j, each row added under lane mask j. The shards of a
+// block (register bits 0-1) share the twiddle and the butterfly pairs whole blocks (D >= 4
+// registers), so each block w[8b..8b+8) is 8 planes (tr8) as in arrangement B.
+template <int LOGK, int D_LOG, bool IFFT, int HS, int NW>
+__device__ __forceinline__ void layer_p(uint32_t (&w)[NW]) {
+  static_assert(D_LOG >= 2 && D_LOG <= 4, "plane layers are 2-4");
+  constexpr uint32_t K = 1u << LOGK;
+  constexpr int NB = NW / 8;
+  constexpr int DB = 1 << (D_LOG - 2);  // block distance
+  constexpr int S = 5 - D_LOG;
+  uint32_t m0, m1, m2;
+  lane_masks(m0, m1, m2);
+  const uint32_t M[8] = {0u, m0, m1, m0 ^ m1, m2, m0 ^ m2, m1 ^ m2, m0 ^ m1 ^ m2};  // M[J]: parity of L & J
+  sfor<NB / (2 * DB)>([&](auto gi) {
+    constexpr int b0 = decltype(gi)::value * 2 * DB;
+    if constexpr (in_half<HS, b0>()) {
+      constexpr uint32_t sb = shard_bits_a<LOGK>(4u * b0);
+      constexpr uint32_t c = IFFT ? ifft_tw(K, D_LOG, sb) : fft_tw(D_LOG, sb);
+      static_assert(coord_b(c) == 0, "plane layers need twiddles in GF(2^8)");
+      sfor<DB>([&](auto ji) {
+        constexpr int x = 8 * (b0 + decltype(ji)::value), y = x + 8 * DB;
+        if constexpr (IFFT) pxor<x, y>(w);
+        pmuladd_lane<coord_a(c), S, x, y>(w, M);
+        if constexpr (!IFFT) pxor<x, y>(w);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    }
+  });
+}
+
+// bytes <-> bit planes for every block of half HS (all if HS < 0)
+template <int HS, int NW>
+__device__ __forceinline__ void tr_blocks(uint32_t (&w)[NW]) {
+  sfor<NW / 8>([&](auto b) {
+    if constexpr (in_half<HS, decltype(b)::value>()) {
+      tr8<8 * decltype(b)::value>(w);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  });
+}
+
 // Register bit RB (2, 3, 4) <-> lane bit RB + 1 (8, 16, 32 lanes apart): a 2x2 transpose
 // of every register pair (r, r | 1 << RB), for both coordinates. An involution. HS >= 0:
 // the registers of half HS (register bit 5) only.
@@ -255,32 +365,15 @@ __device__ __forceinline__ void swap_bit(uint32_t (&w)[NW]) {
   });
 }
 
-// planes w[XO..XO+8) ^= C * planes w[YO..YO+8) (C < 256; C == 0 adds nothing)
-template <uint32_t C, int XO, int YO, int NW>
-__device__ __forceinline__ void pmuladd(uint32_t (&w)[NW]) {
-  if constexpr (C != 0) {
-    sfor<8>([&](auto r) { xrow<mul_row8(C, decltype(r)::value), YO, 0>(w[XO + decltype(r)::value], w); });
-  }
-}
-
 // Arrangement B: block b = registers 4b..4b+3 = w[8b..8b+8), shard bits 5.. = b; block b
-// lies in half b >> 3 (register bit 5). stage_b_in: the bit transposes and the IFFT layers
-// 5 .. LOGK-2 (block groups of at most 8, inside one half), for half HS (all if HS < 0);
-// stage_b_mid: the merged last-IFFT / first-FFT layer (K = 512: across the halves);
-// stage_b_out: the FFT layers LOGK-2 .. 5 and the transposes back, for half HS.
-template <int HS, int B>
-constexpr bool in_half() { return HS < 0 || (B >> 3) == HS; }
-
+// lies in half b >> 3 (register bit 5); the blocks are already bit planes (tr_blocks before
+// layer 2). stage_b_in: the IFFT layers 5 .. LOGK-2 (block groups of at most 8, inside one
+// half), for half HS (all if HS < 0); stage_b_mid: the merged last-IFFT / first-FFT layer
+// (K = 512: across the halves); stage_b_out: the FFT layers LOGK-2 .. 5, for half HS.
 template <int LOGK, int HS, int NW>
 __device__ __forceinline__ void stage_b_in(uint32_t (&w)[NW]) {
   constexpr uint32_t K = 1u << LOGK;
   constexpr int NB = NW / 8;
-  sfor<NB>([&](auto b) {
-    if constexpr (in_half<HS, decltype(b)::value>()) {
-      tr8<8 * decltype(b)::value>(w);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  });
   // IFFT layers 5 .. LOGK-2
   sfor<LOGK - 6>([&](auto t) {
     constexpr int d = 5 + decltype(t)::value;
@@ -335,12 +428,6 @@ __device__ __forceinline__ void stage_b_out(uint32_t (&w)[NW]) {
         });
       }
     });
-  });
-  sfor<NB>([&](auto b) {
-    if constexpr (in_half<HS, decltype(b)::value>()) {
-      tr8<8 * decltype(b)::value>(w);
-      __builtin_amdgcn_sched_barrier(0);
-    }
   });
 }
 
@@ -462,9 +549,10 @@ __global__ __launch_bounds__(256, LOGK == 9 ? 3 : 4) void k_rs_gf16x(RsGeom g) {
     // IFFT, arrangement A
     layer_a<LOGK, 0, true, HS>(w, lane_tab_here<5>(), m7, m3);
     layer_a<LOGK, 1, true, HS>(w, lane_tab_here<4>(), m7, m3);
-    layer_a<LOGK, 2, true, HS>(w, lane_tab_here<3>(), m7, m3);
-    layer_a<LOGK, 3, true, HS>(w, lane_tab_here<2>(), m7, m3);
-    layer_a<LOGK, 4, true, HS>(w, lane_tab_here<1>(), m7, m3);
+    tr_blocks<HS>(w);  // -> bit planes
+    layer_p<LOGK, 2, true, HS>(w);
+    layer_p<LOGK, 3, true, HS>(w);
+    layer_p<LOGK, 4, true, HS>(w);
     swap_bit<2, HS>(w);
     swap_bit<3, HS>(w);
     swap_bit<4, HS>(w);
@@ -480,9 +568,10 @@ __global__ __launch_bounds__(256, LOGK == 9 ? 3 : 4) void k_rs_gf16x(RsGeom g) {
     swap_bit<3, HS>(w);
     swap_bit<4, HS>(w);
     // FFT, arrangement A
-    layer_a<LOGK, 4, false, HS>(w, lane_tab_here<1>(), m7, m3);
-    layer_a<LOGK, 3, false, HS>(w, lane_tab_here<2>(), m7, m3);
-    layer_a<LOGK, 2, false, HS>(w, lane_tab_here<3>(), m7, m3);
+    layer_p<LOGK, 4, false, HS>(w);
+    layer_p<LOGK, 3, false, HS>(w);
+    layer_p<LOGK, 2, false, HS>(w);
+    tr_blocks<HS>(w);  // -> bytes
     layer_a<LOGK, 1, false, HS>(w, lane_tab_here<4>(), m7, m3);
     layer_a<LOGK, 0, false, HS>(w, lane_tab_here<5>(), m7, m3);
     convert<HS>(w, m7, m3);  // -> (lo, hi)
