@@ -238,18 +238,42 @@ __device__ __forceinline__ void lane_masks(uint32_t& m0, uint32_t& m1, uint32_t&
 
 // Row R of x ^= (CA + lane part) * y, the lane part sum_j L_j * (1 << (S + j)): the
 // coefficient of plane y_k is c0 ^ parity(L & J) (c0 = bit k of CA's row, J = the e_j whose
-// rows have bit k). lane_group(key) = the planes k whose (J, c0) is (key >> 1, key & 1).
-template <uint32_t CA, int S, int R>
-constexpr uint32_t lane_group(int key) {
-  uint32_t g = 0;
-  for (int k = 0; k < 8; k++) {
-    uint32_t J = 0;
-    for (int j = 0; j < 3; j++) J |= ((mul_row8((1u << j) << S, R) >> k) & 1u) << j;
-    const uint32_t c0 = (mul_row8(CA, R) >> k) & 1u;
-    if ((int)(J * 2 + c0) == key) g |= 1u << k;
+// rows have bit k). g[R][key] = the planes k whose (J, c0) is (key >> 1, key & 1). One table
+// per (CA, S), evaluated once (a static constexpr member), so the compile stays short.
+struct LaneGroupTab {
+  uint32_t g[8][16];
+};
+constexpr LaneGroupTab make_lane_groups(uint32_t CA, int S) {
+  LaneGroupTab t{};
+  for (int R = 0; R < 8; R++) {
+    const uint32_t rc = mul_row8(CA, R);
+    const uint32_t r0 = mul_row8(1u << S, R), r1 = mul_row8(2u << S, R), r2 = mul_row8(4u << S, R);
+    for (int k = 0; k < 8; k++) {
+      const uint32_t J = ((r0 >> k) & 1u) | (((r1 >> k) & 1u) << 1) | (((r2 >> k) & 1u) << 2);
+      t.g[R][J * 2 + ((rc >> k) & 1u)] |= 1u << k;
+    }
   }
-  return g;
+  return t;
 }
+// The classes rebuild "multiply by CA + lane part" for every lane value L (mul_row8 is
+// linear in c; checked at compile time for each (CA, S) the kernel uses).
+constexpr bool lane_groups_ok(const LaneGroupTab& t, uint32_t CA, int S) {
+  for (uint32_t L = 0; L < 8; L++) {
+    const uint32_t c = CA ^ ((L & 1u) << S) ^ ((L & 2u) << S) ^ ((L & 4u) << S);
+    for (int R = 0; R < 8; R++) {
+      uint32_t row = 0;
+      for (int key = 1; key < 16; key++)
+        if (((uint32_t)key & 1u) ^ (__builtin_popcount(L & ((uint32_t)key >> 1)) & 1u)) row |= t.g[R][key];
+      if (row != mul_row8(c, R)) return false;
+    }
+  }
+  return true;
+}
+template <uint32_t CA, int S>
+struct LaneGroups {
+  static constexpr LaneGroupTab tab = make_lane_groups(CA, S);
+  static_assert(lane_groups_ok(tab, CA, S), "coefficient classes do not rebuild the product");
+};
 
 // planes w[XO..XO+8) ^= (CA + lane part) * planes w[YO..YO+8): per row, the planes of one
 // coefficient class are XORed together and added under that class's lane mask M[J] (or its
@@ -260,7 +284,7 @@ __device__ __forceinline__ void pmuladd_lane(uint32_t (&w)[NW], const uint32_t (
     constexpr int r = decltype(ri)::value;
     sfor<16>([&](auto ki) {
       constexpr int key = decltype(ki)::value;
-      constexpr uint32_t g = lane_group<CA, S, r>(key);
+      constexpr uint32_t g = LaneGroups<CA, S>::tab.g[r][key];
       if constexpr (key == 1 && g != 0) {
         xrow<g, YO, 0>(w[XO + r], w);
       } else if constexpr (key > 1 && g != 0) {
@@ -295,15 +319,12 @@ constexpr bool in_half() { return HS < 0 || (B >> 3) == HS; }
 // block (register bits 0-1) share the twiddle and the butterfly pairs whole blocks (D >= 4
 // registers), so each block w[8b..8b+8) is 8 planes (tr8) as in arrangement B.
 template <int LOGK, int D_LOG, bool IFFT, int HS, int NW>
-__device__ __forceinline__ void layer_p(uint32_t (&w)[NW]) {
+__device__ __forceinline__ void layer_p(uint32_t (&w)[NW], const uint32_t (&M)[8]) {
   static_assert(D_LOG >= 2 && D_LOG <= 4, "plane layers are 2-4");
   constexpr uint32_t K = 1u << LOGK;
   constexpr int NB = NW / 8;
   constexpr int DB = 1 << (D_LOG - 2);  // block distance
   constexpr int S = 5 - D_LOG;
-  uint32_t m0, m1, m2;
-  lane_masks(m0, m1, m2);
-  const uint32_t M[8] = {0u, m0, m1, m0 ^ m1, m2, m0 ^ m2, m1 ^ m2, m0 ^ m1 ^ m2};  // M[J]: parity of L & J
   sfor<NB / (2 * DB)>([&](auto gi) {
     constexpr int b0 = decltype(gi)::value * 2 * DB;
     if constexpr (in_half<HS, b0>()) {
@@ -550,9 +571,12 @@ __global__ __launch_bounds__(256, LOGK == 9 ? 3 : 4) void k_rs_gf16x(RsGeom g) {
     layer_a<LOGK, 0, true, HS>(w, lane_tab_here<5>(), m7, m3);
     layer_a<LOGK, 1, true, HS>(w, lane_tab_here<4>(), m7, m3);
     tr_blocks<HS>(w);  // -> bit planes
-    layer_p<LOGK, 2, true, HS>(w);
-    layer_p<LOGK, 3, true, HS>(w);
-    layer_p<LOGK, 4, true, HS>(w);
+    uint32_t m0, m1, m2;
+    lane_masks(m0, m1, m2);
+    const uint32_t M[8] = {0u, m0, m1, m0 ^ m1, m2, m0 ^ m2, m1 ^ m2, m0 ^ m1 ^ m2};  // M[J]: parity of L & J
+    layer_p<LOGK, 2, true, HS>(w, M);
+    layer_p<LOGK, 3, true, HS>(w, M);
+    layer_p<LOGK, 4, true, HS>(w, M);
     swap_bit<2, HS>(w);
     swap_bit<3, HS>(w);
     swap_bit<4, HS>(w);
@@ -568,9 +592,12 @@ __global__ __launch_bounds__(256, LOGK == 9 ? 3 : 4) void k_rs_gf16x(RsGeom g) {
     swap_bit<3, HS>(w);
     swap_bit<4, HS>(w);
     // FFT, arrangement A
-    layer_p<LOGK, 4, false, HS>(w);
-    layer_p<LOGK, 3, false, HS>(w);
-    layer_p<LOGK, 2, false, HS>(w);
+    uint32_t m0, m1, m2;
+    lane_masks(m0, m1, m2);
+    const uint32_t M[8] = {0u, m0, m1, m0 ^ m1, m2, m0 ^ m2, m1 ^ m2, m0 ^ m1 ^ m2};  // M[J]: parity of L & J
+    layer_p<LOGK, 4, false, HS>(w, M);
+    layer_p<LOGK, 3, false, HS>(w, M);
+    layer_p<LOGK, 2, false, HS>(w, M);
     tr_blocks<HS>(w);  // -> bytes
     layer_a<LOGK, 1, false, HS>(w, lane_tab_here<4>(), m7, m3);
     layer_a<LOGK, 0, false, HS>(w, lane_tab_here<5>(), m7, m3);
