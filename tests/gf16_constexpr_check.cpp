@@ -72,6 +72,34 @@ int main() {
       if (bits != mul(c, y)) { printf("mul_row8 %u %u\n", c, y); return 1; }
     }
   }
+  // rs_gf16x layer_p (layers 2-4, arrangement A): the encoder's twiddle of a butterfly whose
+  // group base s has lane bits L (shard bits 5-7) is ca ^ L << (5 - m), ca the twiddle of the
+  // same base with L = 0, all in GF(2^8) (coord_b 0); so x ^= c*y is ca*y plus the lane bits'
+  // products. Checked against the oracle's skew table and field for K = 256, 512, both the
+  // IFFT (block base K + s) and the FFT (base s).
+  for (unsigned K = 256; K <= 512; K *= 2)
+    for (int m = 2; m <= 4; m++)
+      for (int fft = 0; fft < 2; fft++)
+        for (unsigned s = 0; s < K; s += 2u << m) {
+          const unsigned B = fft ? s : K + s, B0 = fft ? (s & ~0xE0u) : K + (s & ~0xE0u), L = (s >> 5) & 7u;
+          const int e = orc_gf_skew(16, (int)((1u << m) - 1 + B)), e0 = orc_gf_skew(16, (int)((1u << m) - 1 + B0));
+          const unsigned c = e == 65535 ? 0u : (unsigned)orc_gf_exp(16, e);
+          const unsigned c0 = e0 == 65535 ? 0u : (unsigned)orc_gf_exp(16, e0);
+          if (coord_b(c) != 0 || c != (c0 ^ (L << (5 - m)))) {
+            printf("layer_p twiddle K=%u m=%d fft=%d s=%u: %u vs %u ^ lane\n", K, m, fft, s, c, c0);
+            return 1;
+          }
+          for (int t = 0; t < 8; t++) {
+            const unsigned y = rnd();
+            unsigned v = (unsigned)orc_gf_mul(16, (int)c0, (int)y);
+            for (int j = 0; j < 3; j++)
+              if ((L >> j) & 1u) v ^= (unsigned)orc_gf_mul(16, (int)((1u << j) << (5 - m)), (int)y);
+            if (v != (unsigned)orc_gf_mul(16, (int)c, (int)y)) {
+              printf("layer_p lane product K=%u m=%d s=%u\n", K, m, s);
+              return 1;
+            }
+          }
+        }
   printf("ok p=%u q=%u\n", kP, kQ);
   return 0;
 }

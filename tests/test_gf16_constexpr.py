@@ -1,6 +1,7 @@
 """The compile-time GF(2^16) arithmetic of the GF(2^16) encoder (gf16_constexpr.hpp) is
 the oracle's field: products, the twiddle = index structure of the skew table, the
-GF(2^8) subfield and (a, b) coordinates, and the v_perm / bit-matrix tables. Host only."""
+GF(2^8) subfield and (a, b) coordinates, the v_perm / bit-matrix tables, and the lane
+decomposition of the twiddles the plane layers 2-4 rely on (rs_gf16x.hip layer_p). Host only."""
 import os
 import subprocess
 
